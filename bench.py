@@ -1,0 +1,264 @@
+"""Benchmark of the flash-attention forward on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+    python bench.py --mode splitkv-dist ...   (C5: one sequence's keys sharded over ranks)
+
+Default workload (N=1): config C3 of BASELINE.json -- FA-v1 fused forward, B=32 H=8 L=1024
+d=128, bf16 storage / fp32 accumulate, synthetic N(0,1) inputs resident in HBM.  A step
+is one forward over the whole batch.  With N>1 every rank runs its own C3 batch (heads
+are independent units: weak scaling, no collective in the data path).
+
+Prints ONE JSON line on rank 0 with the metric, the MFMA roofline of the forward kernel
+(achieved = 4*B*H*L^2*d FLOPs per launch / average launch time from HIP events on the
+launch stream) and the CPU baseline: the oracle's restatement of the reference's
+flash_attention_v1/numpy_gpu_like_opt2.py (fp64, Bq=Bk=8) timed on a bounded sample of the
+same workload's heads, one head per process, on the host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md)
+CONFIGS = {
+    "c2": dict(B=32, H=8, L=1024, d=32, variant="v1"),
+    "c3": dict(B=32, H=8, L=1024, d=128, variant="v1"),
+    "c4": dict(B=32, H=8, L=4096, d=128, variant="v2", kvtpb=4),
+    "c5": dict(B=32, H=8, L=16384, d=128, variant="dist"),
+}
+
+
+def flops(B, H, L, d, Lk=None):
+    return 4.0 * B * H * L * (L if Lk is None else Lk) * d
+
+
+# ------------------------------------------------------------------------------------
+# CPU baseline (oracle restatement of numpy_gpu_like_opt2.py), run BEFORE any GPU init
+# ------------------------------------------------------------------------------------
+
+def _cpu_head(args):
+    L, d, seed = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    import numpy as np
+    from oracle.fa_v1 import flash_attention_tiled_flat
+    rng = np.random.default_rng(seed)
+    Q, K, V = (rng.standard_normal(L * d) for _ in range(3))
+    O = np.zeros(L * d)
+    t0 = time.perf_counter()
+    flash_attention_tiled_flat(Q, K, V, O, L, d, Bq=8, Bk=8)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(L, d, heads):
+    import multiprocessing as mp
+    for var in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[var] = "1"
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(heads) as pool:
+        per_head = pool.map(_cpu_head, [(L, d, s) for s in range(heads)])
+    wall = time.perf_counter() - t0
+    return {
+        "value": round(heads * flops(1, 1, L, d) / wall / 1e9, 4),
+        "unit": "GFLOP/s",
+        "cores": heads,
+        "kind": "port",
+        "sample": (f"{heads} heads of L={L} d={d} (fp64, Bq=Bk=8), one head per process on "
+                   f"{heads} host cores; wall {wall:.1f} s, {sum(per_head) / heads:.1f} s per head; "
+                   f"restatement of flash_attention_v1/numpy_gpu_like_opt2.py (oracle/fa_v1.py)"),
+    }
+
+
+# ------------------------------------------------------------------------------------
+# GPU timing
+# ------------------------------------------------------------------------------------
+
+def _make_inputs(torch, dev, B, H, L, d, seed, Lk=None):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    Lk = L if Lk is None else Lk
+    q = torch.randn(B, H, L, d, device=dev, dtype=torch.bfloat16, generator=g)
+    k = torch.randn(B, H, Lk, d, device=dev, dtype=torch.bfloat16, generator=g)
+    v = torch.randn(B, H, Lk, d, device=dev, dtype=torch.bfloat16, generator=g)
+    return q, k, v
+
+
+def time_step(torch, step, steps, warmup, barrier):
+    """Warm up, then time exactly `steps` calls.  Returns (wall_s, event_ms_total)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    return wall, ev0.elapsed_time(ev1)
+
+
+def load_traffic(config):
+    path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(config)
+        return None if rec is None else rec.get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--mode", default="heads", choices=["heads", "splitkv-dist"])
+    ap.add_argument("--cpu-heads", type=int, default=0, help="CPU baseline sample (0 = min(16, cores))")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the per-variant extra timings")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    cfg = CONFIGS["c5"] if args.mode == "splitkv-dist" else CONFIGS[args.config]
+    B, H, L, d = cfg["B"], cfg["H"], cfg["L"], cfg["d"]
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "heads":
+        heads = args.cpu_heads or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(L, d, heads)  # before any GPU initialisation (fork-safe)
+
+    import torch
+    import torch.distributed as dist
+
+    from exploring_flash_attention_amd import dist as fdist
+    from exploring_flash_attention_amd import ops
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    extra = {}
+    if args.mode == "heads":
+        q, k, v = _make_inputs(torch, dev, B, H, L, d, seed=1234 + rank)
+        out = torch.empty_like(q)
+        if cfg["variant"] == "v1":
+            def step():
+                ops.attention_v1(q, k, v, out=out)
+            kernel = "fa_fwd_kernel (final)"
+        else:
+            nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype, q.dtype)
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+
+            def step():
+                ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
+            kernel = "fa_fwd_kernel (partial) + fa_combine_kernel"
+        wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
+        work = flops(B, H, L, d)
+        workload = f"FA-{'v1 fused' if cfg['variant'] == 'v1' else 'v2 split-KV'} forward"
+        parallel = f"heads{world}" if world > 1 else "single"
+    else:
+        # C5: keys of one L=16384 sequence sharded over the ranks; all-to-all combine.
+        lo, hi = fdist.shard_bounds(L, world, rank)
+        q, _, _ = _make_inputs(torch, dev, B, H, L, d, seed=99)  # same Q on every rank
+        _, k, v = _make_inputs(torch, dev, B, H, 1, d, seed=1000 + rank, Lk=hi - lo)
+
+        def step():
+            fdist.splitkv_attention(q, k, v)
+        wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
+        work = flops(B, H, L, d, Lk=hi - lo)  # this rank's share
+        kernel = "fa_fwd_kernel (partial) + all_to_all + fa_combine_kernel"
+        workload = "FA-v2 split-KV forward, keys sharded over ranks"
+        parallel = f"kv{world}"
+
+    # max over ranks
+    t = torch.tensor([wall, ev_ms], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, ev_ms = float(t[0]), float(t[1])
+    ms_per_step = wall / args.steps * 1e3
+    total_work = work * world
+    value = total_work / (wall / args.steps) / 1e9
+
+    if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
+        # per-variant timings at N=1 (informational; not the headline value)
+        for name, c, fn in (("c3_tiled_d", "c3", "tiled_d"), ("c2_fused", "c2", "v1"),
+                            ("c4_splitkv", "c4", "v2")):
+            cc = CONFIGS[c]
+            qq, kk, vv = _make_inputs(torch, dev, cc["B"], cc["H"], cc["L"], cc["d"], seed=7)
+            if fn == "tiled_d":
+                def st():
+                    ops.attention_tiled_d(qq, kk, vv, 32, 32)
+            elif fn == "v1":
+                def st():
+                    ops.attention_v1(qq, kk, vv)
+            else:
+                nb, _ = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], 4, qq.dtype, qq.dtype)
+                wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
+
+                def st():
+                    ops.attention_v2(qq, kk, vv, 4, workspace=wsx)
+            n = 20
+            _, ems = time_step(torch, st, n, 5, barrier)
+            f = flops(cc["B"], cc["H"], cc["L"], cc["d"])
+            extra[name] = {"ms": round(ems / n, 4), "tflops": round(f / (ems / n * 1e-3) / 1e12, 1)}
+            del qq, kk, vv
+
+    if rank == 0:
+        avg_ms = ev_ms / args.steps
+        achieved = work / (avg_ms * 1e-3) / 1e12
+        traffic = load_traffic(args.config if args.mode == "heads" else "c5")
+        line = {
+            "metric": "flash-attn fwd GFLOP/s (B=32,H=8,L=1024,d=128; % MFMA roofline)"
+            if args.mode == "heads" and args.config == "c3" else f"flash-attn fwd GFLOP/s ({args.config if args.mode == 'heads' else 'c5'})",
+            "value": round(value, 1),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic N(0,1)",
+            "config": {"workload": workload, "B": B, "H": H, "L": L, "d": d,
+                       "global_batch": B * H * world, "seq_len": L, "parallelism": parallel,
+                       "tiles": {"bq": 128, "bk": 64, "threads": 256}},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                         "traffic": traffic, "kernel": kernel,
+                         "kernel_ms": round(avg_ms, 5)},
+            "cpu_baseline": cpu,
+        }
+        if extra:
+            line["extra"] = extra
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,351 @@
+// fa_fwd.hip -- flash-attention forward for MI355X (gfx950 / CDNA4).
+//
+// One kernel template serves the three reference kernel families:
+//   final mode   (PARTIAL=false): FA-v1 fused / d-tiled forward
+//                 <- flash_attention_kernel    flash_attention_v1/CUDA/flash_attention_v1.h:161
+//                 <- flash_attention_kernel_opt1 flash_attention_v1/CUDA/flash_attention_v1_opt1.h:264
+//                 <- flash_attention_kernel (tiled-d) flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:230
+//   partial mode (PARTIAL=true): FA-v2 split-KV partial kernel
+//                 <- partial_attention_kernel  flash_attention_v2/CUDA/flash_attention_v2.h:243
+//
+// Online-softmax recurrence per KV tile (flash_attention_v1/numpy_gpu_like_opt2.py:135-195):
+//   S = Q K^T * scale; m_new = max(m, rowmax S); alpha = e^(m - m_new);
+//   P = e^(S - m_new); l = l*alpha + rowsum P; O = O*alpha + P V;  finally O / l.
+// Here the exponentials are base 2 with log2(e)/sqrt(d) folded into one FMA.
+//
+// Mapping to CDNA4 (see DESIGN.md for the derivation):
+//   * workgroup = 4 waves x 32 query rows = 128 rows of one (b,h); KV tiles of 64 keys.
+//   * S^T = K . Q^T on v_mfma_f32_32x32x16 (A = K rows from LDS via ds_read_b128,
+//     B = Q^T fragments held in VGPRs for the whole KV loop): the accumulator puts one
+//     query row per lane (lanes l and l+32 share a row), so row max / row sum are
+//     in-lane plus one v_permlane32_swap.
+//   * O^T = V^T . P^T: the S accumulator, exponentiated and packed to 16-bit, is already
+//     the B operand (no LDS round trip); V^T fragments come from ds_read_b64_tr_b16
+//     transposed LDS reads.  O_acc stays in VGPRs/AGPRs for the whole KV loop.
+//   * K and V tiles are register-staged (global_load_dwordx4 issued before the tile's
+//     MFMAs, ds_write_b128 after them) into a double-buffered, XOR-swizzled LDS image
+//     that is bank-conflict-free for both the row reads and the transposed reads.
+//   * blockIdx is remapped so that all query tiles of one (b,h) land on one XCD and
+//     share that head's K/V in the XCD's L2.
+#include "fa_internal.hpp"
+
+namespace fa {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct Mma;
+template <> struct Mma<__bf16> {
+    typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+    static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct Mma<_Float16> {
+    typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+    static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// XOR swizzle of the 16-byte chunk index inside one LDS row of D 16-bit elements.
+// Chosen so that (a) the ds_read_b128 row reads of the 32x32x16 A operand (16 distinct
+// rows per lane group, one chunk) and (b) the ds_read_b64_tr_b16 transposed reads
+// (4 consecutive rows x 32 columns per 32-lane half) both hit 16 distinct 16-byte bank
+// slots, i.e. are conflict-free.  DESIGN.md section "LDS image" has the proof sketch.
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+    if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+    else if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+    else return (row >> 2) & 3;  // D == 32
+}
+
+template <int D>
+__device__ __forceinline__ int lds_off(int row, int chunk) {
+    return row * (D * 2) + 16 * (chunk ^ swz<D>(row));
+}
+
+// Bijective workgroup remap: blocks b and b+8 share an XCD (observed round-robin
+// dispatch, speed only -- results never depend on it), so give each group of blocks
+// with equal b % 8 a contiguous range of work items.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+__device__ __forceinline__ float pair_max(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <typename T>
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+    T x = static_cast<T>(a), y = static_cast<T>(b);
+    return (unsigned)__builtin_bit_cast(unsigned short, x) |
+           ((unsigned)__builtin_bit_cast(unsigned short, y) << 16);
+}
+
+template <typename T, typename PT, int D, bool PARTIAL>
+__global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
+    using M = Mma<T>;
+    using v8 = typename M::v8;
+    constexpr int ROWB = D * 2;               // bytes per LDS row
+    constexpr int NCH = D / 8;                // 16-byte chunks per row
+    constexpr int TILEB = kBK * ROWB;         // bytes of one K (or V) tile
+    constexpr int CPT = kBK * NCH / kThreads; // staged chunks per thread per tile
+    constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
+    constexpr int NDB = D / 32;               // 32-column blocks of O
+    static_assert(kBK * NCH % kThreads == 0, "tile must split evenly over threads");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int qt = w % a.nqt;
+    const int rest = w / a.nqt;
+    const int split = rest % a.nsplit;
+    const int64_t bh = rest / a.nsplit;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int l32 = lane & 31;
+    const int hf = lane >> 5;
+
+    const int64_t kv_begin = (int64_t)split * a.kv_per_split;
+    const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
+    const int ntiles = (int)((kv_end - kv_begin + kBK - 1) / kBK);
+
+    const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D;
+    const unsigned short* Kh = (const unsigned short*)a.k + bh * a.Lk * D;
+    const unsigned short* Vh = (const unsigned short*)a.v + bh * a.Lk * D;
+
+    // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7].
+    const int64_t q_row = (int64_t)qt * kBQ + wid * kRowsPerWave + l32;
+    const int64_t q_row_c = q_row < a.Lq ? q_row : a.Lq - 1;
+    v8 qf[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        u32x4 raw = *(const u32x4*)(Qh + q_row_c * D + ks * 16 + hf * 8);
+        qf[ks] = __builtin_bit_cast(v8, raw);
+    }
+
+    // Register staging of the K and V tiles: thread t moves 16-byte chunks
+    // t, t + kThreads, ... of the [kBK][D] tile (coalesced global reads).
+    u32x4 kst[CPT], vst[CPT];
+    auto stage_load = [&](int64_t kv0) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int idx = tid + i * kThreads;
+            const int row = idx / NCH, ch = idx % NCH;
+            int64_t g = kv0 + row;
+            g = g < kv_end ? g : kv_end - 1;  // clamp: padded keys are masked to -inf
+            kst[i] = *(const u32x4*)(Kh + g * D + ch * 8);
+            vst[i] = *(const u32x4*)(Vh + g * D + ch * 8);
+        }
+    };
+    auto stage_write = [&](int buf) {
+        char* kb = smem + buf * 2 * TILEB;
+        char* vb = kb + TILEB;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int idx = tid + i * kThreads;
+            const int row = idx / NCH, ch = idx % NCH;
+            const int off = lds_off<D>(row, ch);
+            *(u32x4*)(kb + off) = kst[i];
+            *(u32x4*)(vb + off) = vst[i];
+        }
+    };
+
+    f32x16 o[NDB];
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) o[db] = f32x16{};
+    float m = -INFINITY;  // running max, in units of log2 (scores * scale_log2)
+    float l = 0.f;        // this lane's half of the running denominator
+    const float c = a.scale_log2;
+
+    // transposed-read geometry (constant per lane)
+    const int grp = lane >> 4, gi = lane & 15;
+    const int tr_row = 4 * (grp >> 1) + (gi >> 2);
+    const int tr_col = 16 * (grp & 1) + 4 * (gi & 3);
+
+    stage_load(kv_begin);
+    stage_write(0);
+    __syncthreads();
+
+    for (int t = 0; t < ntiles; ++t) {
+        const int64_t kv0 = kv_begin + (int64_t)t * kBK;
+        const bool has_next = t + 1 < ntiles;
+        if (has_next) stage_load(kv0 + kBK);
+        const char* kb = smem + (t & 1) * 2 * TILEB;
+        const char* vb = kb + TILEB;
+
+        // S^T[key][q] for 2 blocks of 32 keys
+        f32x16 s[2];
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2) {
+            s[b2] = f32x16{};
+            const int row = b2 * 32 + l32;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const v8 kf = *(const v8*)(kb + lds_off<D>(row, 2 * ks + hf));
+                s[b2] = M::mma(kf, qf[ks], s[b2]);
+            }
+        }
+
+        // mask keys past the end of this split (only the last, partial tile)
+        if (kv_end - kv0 < kBK) {
+            const int valid = (int)(kv_end - kv0);
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = b2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+                    if (key >= valid) s[b2][r] = -INFINITY;
+                }
+        }
+
+        float mx = s[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
+        mx = pair_max(mx);
+        const float m_new = fmaxf(m, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m - m_new);
+        m = m_new;
+
+        float sum = 0.f;
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[b2][r], c, -m_new));
+                s[b2][r] = p;
+                sum += p;
+            }
+        l = l * alpha + sum;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+
+        // P^T packed to 16-bit: registers 8*ss .. 8*ss+7 of block b2 form the B operand
+        // of k-step ss; its element j is key 16*ss + 8*(j>>2) + 4*hf + (j&3) of the block.
+        v8 pb[2][2];
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                u32x4 u;
+                u[0] = pack2<T>(s[b2][8 * ss + 0], s[b2][8 * ss + 1]);
+                u[1] = pack2<T>(s[b2][8 * ss + 2], s[b2][8 * ss + 3]);
+                u[2] = pack2<T>(s[b2][8 * ss + 4], s[b2][8 * ss + 5]);
+                u[3] = pack2<T>(s[b2][8 * ss + 6], s[b2][8 * ss + 7]);
+                pb[b2][ss] = __builtin_bit_cast(v8, u);
+            }
+
+        // O^T[dv][q] += V^T[dv][key] . P^T[key][q]; the A operand's element j must be
+        // the same key as pb's element j: two transposed reads of 4 keys each.
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int row = b2 * 32 + 16 * ss + tr_row;
+                    const int col = db * 32 + tr_col;
+                    const int sub = (col & 7) * 2;  // 0 or 8 bytes inside the chunk
+                    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(vb + lds_off<D>(row, col >> 3) + sub));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(vb + lds_off<D>(row + 8, col >> 3) + sub));
+                    const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    o[db] = M::mma(__builtin_bit_cast(v8, vv), pb[b2][ss], o[db]);
+                }
+        }
+
+        if (has_next) stage_write((t + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (r&3) + 8*(r>>2) + 4*hf
+    const float l_tot = pair_sum(l);
+    const float inv = 1.f / l_tot;
+    if (q_row >= a.Lq) return;
+    if constexpr (!PARTIAL) {
+        unsigned short* Oh = (unsigned short*)a.o + bh * a.Lq * D + q_row * D;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                u32x2 u;
+                u[0] = pack2<T>(o[db][4 * g4 + 0] * inv, o[db][4 * g4 + 1] * inv);
+                u[1] = pack2<T>(o[db][4 * g4 + 2] * inv, o[db][4 * g4 + 3] * inv);
+                *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
+            }
+    } else {
+        const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
+        const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
+        PT* Op = (PT*)a.o + split * a.split_stride + row_lin * D;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int col = db * 32 + 8 * g4 + 4 * hf;
+                if constexpr (sizeof(PT) == 4) {
+                    f32x4 f = {o[db][4 * g4 + 0] * inv, o[db][4 * g4 + 1] * inv,
+                               o[db][4 * g4 + 2] * inv, o[db][4 * g4 + 3] * inv};
+                    *(f32x4*)(Op + col) = f;
+                } else {
+                    u32x2 u;
+                    u[0] = pack2<T>(o[db][4 * g4 + 0] * inv, o[db][4 * g4 + 1] * inv);
+                    u[1] = pack2<T>(o[db][4 * g4 + 2] * inv, o[db][4 * g4 + 3] * inv);
+                    *(u32x2*)((unsigned short*)Op + col) = u;
+                }
+            }
+        if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m + __builtin_amdgcn_logf(l_tot);
+    }
+}
+
+int fwd_lds_bytes(int d) { return 2 * 2 * kBK * d * 2; }
+
+template <typename T, typename PT, int D, bool PARTIAL>
+static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
+    const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
+    const int lds = fwd_lds_bytes(D);
+    hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, PARTIAL>), dim3((unsigned)nblk), dim3(kThreads),
+                       lds, s, a);
+    return hipGetLastError();
+}
+
+template <typename T, typename PT, bool PARTIAL>
+static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
+    switch (d) {
+        case 32: return launch_one<T, PT, 32, PARTIAL>(a, s);
+        case 64: return launch_one<T, PT, 64, PARTIAL>(a, s);
+        case 128: return launch_one<T, PT, 128, PARTIAL>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_fwd(Elem t, Elem pt, int d, bool partial, const FwdArgs& a, hipStream_t s) {
+    if (!partial) {
+        if (t == Elem::BF16) return launch_d<__bf16, __bf16, false>(d, a, s);
+        if (t == Elem::F16) return launch_d<_Float16, _Float16, false>(d, a, s);
+        return hipErrorInvalidValue;
+    }
+    if (t == Elem::BF16 && pt == Elem::BF16) return launch_d<__bf16, __bf16, true>(d, a, s);
+    if (t == Elem::BF16 && pt == Elem::F32) return launch_d<__bf16, float, true>(d, a, s);
+    if (t == Elem::F16 && pt == Elem::F16) return launch_d<_Float16, _Float16, true>(d, a, s);
+    if (t == Elem::F16 && pt == Elem::F32) return launch_d<_Float16, float, true>(d, a, s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace fa

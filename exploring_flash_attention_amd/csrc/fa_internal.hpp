@@ -1,0 +1,50 @@
+// fa_internal.hpp -- shared definitions between the gfx950 kernels (fa_fwd.hip,
+// fa_combine.hip) and the C-ABI dispatch layer (fa_capi.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace fa {
+
+// Keys per KV tile and query rows per wave of the forward kernel.  A wave owns 32
+// query rows (one 32x32x16 MFMA column block); a workgroup has kWaves waves.
+constexpr int kBK = 64;
+constexpr int kRowsPerWave = 32;
+constexpr int kWaves = 4;
+constexpr int kThreads = kWaves * 64;
+constexpr int kBQ = kWaves * kRowsPerWave;
+
+enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2 };
+
+// Arguments of the forward kernel (final and partial modes share one struct).
+struct FwdArgs {
+    const void* q;           // [BH][Lq][D]
+    const void* k;           // [BH][Lk][D]
+    const void* v;           // [BH][Lk][D]
+    void* o;                 // final: [BH][Lq][D] (T); partial: o_part (PT), see below
+    float* lse;              // partial only: log2-sum-exp per row
+    int64_t BH;
+    int64_t Lq;
+    int64_t Lk;
+    int nqt;                 // query tiles per head = ceil(Lq / kBQ)
+    int nsplit;              // key splits per head
+    int kv_per_split;        // keys per split, multiple of kBK (Lk for a single split)
+    int64_t chunk_rows;      // partial: output row chunking (divides Lq)
+    int64_t split_stride;    // partial: elements between splits of o_part
+    float scale_log2;        // log2(e) / sqrt(d)
+};
+
+struct CombineArgs {
+    const void* o_part;      // [nsplit][rows][D] (PT)
+    const float* lse;        // [nsplit][rows]
+    void* o;                 // [rows][D] (T)
+    int64_t rows;            // BH * L
+    int nsplit;
+};
+
+// Launchers (defined in the .hip files).  Return hipSuccess or the launch error.
+hipError_t launch_fwd(Elem t, Elem pt, int d, bool partial, const FwdArgs& a, hipStream_t s);
+hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStream_t s);
+int fwd_lds_bytes(int d);
+
+}  // namespace fa

@@ -1,0 +1,168 @@
+"""Device-tensor operators over the C ABI (torch tensors in HBM, zero-copy).
+
+Every function takes contiguous ``[B, H, L, d]`` bf16 / fp16 tensors on a ROCm device,
+launches on the current HIP stream of that device and returns without synchronising.
+PyTorch is only the plumbing here (device memory, streams); the work is done by the
+gfx950 kernels in libfa_mi355x.so.
+
+Reference launchers these replace (tyler-utah/exploring_flash_attention):
+  attention_v1       flash_attention_v1/CUDA/flash_attention_v1.h:251 (opt1 :354)
+  attention_tiled_d  flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:312 (opt :448)
+  attention_v2       flash_attention_v2/CUDA/flash_attention_v2.h:438 (opt :559)
+  attention_partial  partial_attention_kernel, flash_attention_v2/CUDA/flash_attention_v2.h:243
+  combine            reduction_kernel,         flash_attention_v2/CUDA/flash_attention_v2.h:356
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP32, check, lib
+
+_DTYPES = {torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
+_PDTYPES = {torch.float32: FA_DTYPE_FP32, torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
+
+SUPPORTED_HEAD_DIMS = (32, 64, 128)
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _check_tensor(name, t, dtype=None, device=None, ndim=4):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a ROCm device tensor (got device {t.device}); "
+                         "the MI355X path has no CPU fallback")
+    if t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} has dtype {t.dtype}, expected {dtype}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+
+
+def _check_qkv(q, k, v, same_len=True):
+    _check_tensor("q", q)
+    if q.dtype not in _DTYPES:
+        raise ValueError(f"q dtype {q.dtype} unsupported (bfloat16 or float16)")
+    _check_tensor("k", k, q.dtype, q.device)
+    _check_tensor("v", v, q.dtype, q.device)
+    if k.shape != v.shape:
+        raise ValueError(f"k {tuple(k.shape)} and v {tuple(v.shape)} must have the same shape")
+    if q.shape[0] != k.shape[0] or q.shape[1] != k.shape[1] or q.shape[3] != k.shape[3]:
+        raise ValueError(f"q {tuple(q.shape)} and k {tuple(k.shape)} disagree on B, H or d")
+    if same_len and q.shape != k.shape:
+        raise ValueError(f"q {tuple(q.shape)} and k {tuple(k.shape)} must have the same shape")
+
+
+def _out(out, q, shape=None, dtype=None):
+    shape = tuple(q.shape) if shape is None else shape
+    dtype = q.dtype if dtype is None else dtype
+    if out is None:
+        return torch.empty(shape, dtype=dtype, device=q.device)
+    _check_tensor("out", out, dtype, q.device, ndim=len(shape))
+    if tuple(out.shape) != shape:
+        raise ValueError(f"out has shape {tuple(out.shape)}, expected {shape}")
+    return out
+
+
+def attention_v1(q, k, v, out=None):
+    """FA-v1 fused forward: O = softmax(q k^T / sqrt(d)) v."""
+    _check_qkv(q, k, v)
+    o = _out(out, q)
+    B, H, L, d = q.shape
+    check(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
+    return o
+
+
+def attention_tiled_d(q, k, v, d_tile_qk=32, d_tile_v=32, out=None):
+    """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher."""
+    _check_qkv(q, k, v)
+    o = _out(out, q)
+    B, H, L, d = q.shape
+    check(lib().fa_fwd_v1_tiled_d(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+                                  int(d_tile_v), _DTYPES[q.dtype], _stream(q)))
+    return o
+
+
+def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
+                       partial_dtype=None):
+    """(bytes, num_splits) of the split-KV workspace."""
+    pd = dtype if partial_dtype is None else partial_dtype
+    nbytes = ctypes.c_size_t()
+    ns = ctypes.c_int()
+    check(lib().fa_fwd_v2_workspace_size(B, H, L, d, int(kv_tiles_per_block), _DTYPES[dtype],
+                                         _PDTYPES[pd], ctypes.byref(nbytes), ctypes.byref(ns)))
+    return nbytes.value, ns.value
+
+
+def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, partial_dtype=None,
+                 out=None, workspace=None):
+    """FA-v2 split-KV forward (partial kernel + combine kernel).
+
+    A split is ``kv_tiles_per_block`` KV tiles of the kernel's own tile size (64 keys).
+    ``workspace`` (a uint8 device tensor) is allocated from torch's caching allocator when
+    not given, so the call itself never reaches hipMalloc after warm-up.
+    """
+    _check_qkv(q, k, v)
+    o = _out(out, q)
+    B, H, L, d = q.shape
+    pd = q.dtype if partial_dtype is None else partial_dtype
+    nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
+    if workspace is None:
+        workspace = torch.empty(nbytes, dtype=torch.uint8, device=q.device)
+    elif workspace.numel() * workspace.element_size() < nbytes:
+        raise ValueError(f"workspace too small: {nbytes} bytes needed")
+    check(lib().fa_fwd_v2(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+                          int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace),
+                          workspace.numel() * workspace.element_size(), _DTYPES[q.dtype],
+                          _PDTYPES[pd], _stream(q)))
+    return o
+
+
+def attention_partial(q, k, v, chunk_rows=None, partial_dtype=torch.float32, o_part=None, lse=None):
+    """Split-KV partial over one whole key range (k, v: [B, H, Lk, d]).
+
+    Returns ``(o_part, lse)`` with o_part ``[Lq/chunk_rows, B*H, chunk_rows, d]`` holding the
+    normalised partial output and lse ``[Lq/chunk_rows, B*H, chunk_rows]`` its base-2
+    log-sum-exp (of the scores times log2(e)/sqrt(d)).
+    """
+    _check_qkv(q, k, v, same_len=False)
+    B, H, Lq, d = q.shape
+    Lk = k.shape[2]
+    cr = Lq if chunk_rows is None else int(chunk_rows)
+    if cr <= 0 or Lq % cr:
+        raise ValueError(f"chunk_rows={cr} must divide Lq={Lq}")
+    nch = Lq // cr
+    o_part = _out(o_part, q, (nch, B * H, cr, d), partial_dtype)
+    lse = _out(lse, q, (nch, B * H, cr), torch.float32)
+    check(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
+                               cr, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
+    return o_part, lse
+
+
+def combine(o_part, lse, B, H, dtype, out=None):
+    """Combine ``S`` partials o_part ``[S, B*H, L, d]`` / lse ``[S, B*H, L]`` -> ``[B, H, L, d]``."""
+    _check_tensor("o_part", o_part, ndim=4)
+    _check_tensor("lse", lse, torch.float32, o_part.device, ndim=3)
+    S, BH, L, d = o_part.shape
+    if BH != B * H or tuple(lse.shape) != (S, BH, L):
+        raise ValueError(f"inconsistent shapes o_part {tuple(o_part.shape)} lse {tuple(lse.shape)} "
+                         f"B={B} H={H}")
+    o = _out(out, o_part, (B, H, L, d), dtype)
+    check(lib().fa_combine(_ptr(o_part), _ptr(lse), _ptr(o), S, B, H, L, d, _DTYPES[dtype],
+                           _PDTYPES[o_part.dtype], _stream(o_part)))
+    return o
+
+
+def kernel_geometry(d, dtype=torch.bfloat16):
+    """(bq, bk, threads, lds_bytes) the library uses for head dim d."""
+    return _lib.geometry(d, _DTYPES[dtype])

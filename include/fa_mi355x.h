@@ -1,0 +1,137 @@
+/*
+ * fa_mi355x.h -- C ABI of the MI355X (gfx950) flash-attention forward library
+ * (libfa_mi355x.so, built from exploring_flash_attention_amd/csrc/).
+ *
+ * Computes the exact, non-causal attention forward O = softmax(Q K^T / sqrt(d)) V
+ * over contiguous row-major [B, H, L, d] tensors held in device memory (HBM).
+ * All entry points are asynchronous on the caller's HIP stream (pass NULL for the
+ * null stream), never allocate, never synchronise the device, and return an
+ * fa_status_t.  On failure fa_last_error() returns a thread-local message.
+ *
+ * Each entry point replaces one host launcher of the reference
+ * (tyler-utah/exploring_flash_attention, paths relative to its root):
+ *
+ *   fa_fwd_v1          <- flash_attention_v1(Q,K,V,O,B,H,L,d)
+ *                           flash_attention_v1/CUDA/flash_attention_v1.h:251
+ *                         flash_attention_v1_opt1(Q,K,V,O,B,H,L,d)
+ *                           flash_attention_v1/CUDA/flash_attention_v1_opt1.h:354
+ *   fa_fwd_v1_tiled_d  <- flash_attention_v1(Q,K,V,O,B,H,L,d,d_tile_qk,d_tile_v)
+ *                           flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:312
+ *                         flash_attention_v1_opt(...)
+ *                           flash_attention_v1_tiled_d/CUDA/flash_attention_v1_opt.h:448
+ *   fa_fwd_v2_workspace_size + fa_fwd_v2
+ *                      <- flash_attention_v2(Q,K,V,O,B,H,L,d,d_tile_qk,d_tile_v,kv_tiles_per_block)
+ *                           flash_attention_v2/CUDA/flash_attention_v2.h:438 (opt: _opt.h:559)
+ *                         The reference cudaMallocs/frees its workspace inside every call
+ *                         (flash_attention_v2.h:461-463, :506-508); here the caller owns it.
+ *   fa_fwd_partial     <- partial_attention_kernel  flash_attention_v2/CUDA/flash_attention_v2.h:243
+ *   fa_combine         <- reduction_kernel          flash_attention_v2/CUDA/flash_attention_v2.h:356
+ *                         (exposed separately so a multi-GPU caller can put an RCCL exchange
+ *                         between the two kernels; the reference has no multi-GPU path)
+ *
+ * Differences from the reference contract, all deliberate:
+ *   - the reference launchers return void, assert() on bad arguments and end with
+ *     cudaDeviceSynchronize(); these return a status and never synchronise;
+ *   - the reference element type is __half (or double under USE_FP64); here the
+ *     element type is a runtime argument (FA_DTYPE_BF16 or FA_DTYPE_FP16);
+ *   - the reference fixes the head dim at compile time (assert(d == D),
+ *     flash_attention_v1/CUDA/flash_attention_v1.h:264); here d is dispatched at run
+ *     time to kernels for d in {32, 64, 128}; any other d returns FA_ERR_UNSUPPORTED;
+ *   - sizes are int64_t and every offset is 64-bit (the reference overflows int32 in
+ *     its workspace index at L=4096, flash_attention_v2/CUDA/flash_attention_v2.h:324).
+ */
+#ifndef FA_MI355X_H
+#define FA_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum fa_status {
+    FA_OK = 0,
+    FA_ERR_INVALID_ARG = 1,  /* null pointer, non-positive size, bad tile argument */
+    FA_ERR_UNSUPPORTED = 2,  /* head dim / dtype without a kernel */
+    FA_ERR_HIP = 3,          /* a HIP runtime call failed (launch, attribute) */
+    FA_ERR_WORKSPACE = 4     /* workspace missing or smaller than fa_fwd_v2_workspace_size */
+} fa_status_t;
+
+typedef enum fa_dtype {
+    FA_DTYPE_FP16 = 0,       /* IEEE binary16 storage, fp32 accumulate */
+    FA_DTYPE_BF16 = 1,       /* bfloat16 storage, fp32 accumulate */
+    FA_DTYPE_FP32 = 2        /* only valid as the split-KV partial-output type */
+} fa_dtype_t;
+
+/* Library version, (major << 16) | (minor << 8) | patch. */
+int fa_version(void);
+
+/* Thread-local message describing the last non-FA_OK status on this thread. */
+const char* fa_last_error(void);
+
+/* Geometry the library uses for (d, dtype): query rows per workgroup (*bq),
+ * keys per KV tile (*bk), threads per workgroup (*threads), LDS bytes per workgroup
+ * (*lds_bytes).  Any output pointer may be NULL. */
+int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads,
+                       int* lds_bytes);
+
+/* FA-v1 fused forward.  q, k, v, o: [B, H, L, d] contiguous, element type dtype. */
+int fa_fwd_v1(const void* q, const void* k, const void* v, void* o,
+              int64_t B, int64_t H, int64_t L, int64_t d,
+              int dtype, void* stream);
+
+/* FA-v1 d-tiled forward.  d_tile_qk / d_tile_v must satisfy 0 < d_tile <= d
+ * (the reference's asserts, flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327),
+ * otherwise FA_ERR_INVALID_ARG.  The d-chunking of the arithmetic is set by the MFMA
+ * shape (QK^T accumulates over 16-column k-steps, PV produces 32-column O blocks held
+ * in VGPRs); the tile arguments are validated as the reference does and do not change
+ * the result. */
+int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o,
+                      int64_t B, int64_t H, int64_t L, int64_t d,
+                      int d_tile_qk, int d_tile_v,
+                      int dtype, void* stream);
+
+/* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split is
+ * kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
+ * FA_DTYPE_FP32 or the input dtype.  *num_splits (may be NULL) receives the split count. */
+int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d,
+                             int kv_tiles_per_block, int dtype, int partial_dtype,
+                             size_t* bytes, int* num_splits);
+
+/* FA-v2 split-KV forward: partial kernel over (q-tile, split, b*h), then the combine
+ * kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
+ * 256-byte aligned.  d_tile_qk / d_tile_v as for fa_fwd_v1_tiled_d. */
+int fa_fwd_v2(const void* q, const void* k, const void* v, void* o,
+              int64_t B, int64_t H, int64_t L, int64_t d,
+              int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
+              void* workspace, size_t workspace_bytes,
+              int dtype, int partial_dtype, void* stream);
+
+/* Split-KV partial forward over ONE key range (a whole KV shard, e.g. one GPU's
+ * slice of the sequence).  q: [B, H, Lq, d]; k, v: [B, H, Lk, d].
+ * Writes, for every query row, the normalised partial output and its log-sum-exp
+ * (base 2, of the scaled scores: lse = log2(sum_j 2^(s_j * log2(e)/sqrt(d)))):
+ *   o_part[(row / chunk_rows)][b*H + h][row % chunk_rows][:]   (partial_dtype)
+ *   lse   [(row / chunk_rows)][b*H + h][row % chunk_rows]      (fp32)
+ * chunk_rows must divide Lq.  chunk_rows = Lq gives a plain [B,H,Lq,d] layout;
+ * chunk_rows = Lq / world gives the all-to-all send layout of the multi-GPU path. */
+int fa_fwd_partial(const void* q, const void* k, const void* v,
+                   void* o_part, float* lse,
+                   int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d,
+                   int64_t chunk_rows, int dtype, int partial_dtype, void* stream);
+
+/* Combine num_splits partials: o_part [num_splits][B*H][L][d] (partial_dtype),
+ * lse [num_splits][B*H][L] (fp32, base 2) -> o [B, H, L, d] (dtype), using
+ * O = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M), M = max_s lse_s
+ * (the reference's formula, flash_attention_v2/numpy_gpu_like.py:269-288, on
+ * normalised partials). */
+int fa_combine(const void* o_part, const float* lse, void* o,
+               int64_t num_splits, int64_t B, int64_t H, int64_t L, int64_t d,
+               int dtype, int partial_dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FA_MI355X_H */

@@ -1,0 +1,49 @@
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    """ctypes handle of oracle/_build/liboracle.so (built on demand with gcc)."""
+    import ctypes
+    path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                       stdout=subprocess.DEVNULL)
+    lib = ctypes.CDLL(path)
+    P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    lib.oracle_standard_attention.argtypes = [P, P, P, P, I, I, I, I, I]
+    lib.oracle_driver_random.argtypes = [P, I64, ctypes.c_uint, I]
+    lib.oracle_round_to.argtypes = [P, I64, I]
+    lib.oracle_to_storage.argtypes = [P, P, I64, I]
+    lib.oracle_from_storage.argtypes = [P, P, I64, I]
+    return lib
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """The ROCm device; GPU tests FAIL (not skip) without one -- no silent CPU pass."""
+    import torch
+    assert torch.cuda.is_available(), "GPU test run without a ROCm device"
+    import exploring_flash_attention_amd._lib as L
+    L.lib()  # raises if the HIP library is not built
+    return torch.device("cuda", 0)

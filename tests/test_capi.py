@@ -1,0 +1,128 @@
+"""The C-ABI library loads, exports every symbol include/fa_mi355x.h declares, and
+validates arguments -- CPU only, no kernel launches."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+import exploring_flash_attention_amd._lib as L
+
+HEADER = os.path.join(ROOT, "include", "fa_mi355x.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(fa_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for must in ("fa_fwd_v1", "fa_fwd_v1_tiled_d", "fa_fwd_v2", "fa_fwd_v2_workspace_size",
+                 "fa_fwd_partial", "fa_combine", "fa_last_error", "fa_version", "fa_kernel_geometry"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    h = L.lib()
+    for name in declared_functions():
+        assert hasattr(h, name), f"{name} declared in fa_mi355x.h but not exported"
+    assert set(declared_functions()) == set(L.SIGNATURES), "ctypes SIGNATURES out of sync with header"
+
+
+def test_exports_are_c_symbols_not_mangled():
+    out = os.popen(f"nm -D --defined-only {L.LIB_PATH}").read()
+    for name in declared_functions():
+        assert re.search(rf"\bT {name}$", out, flags=re.M), name
+
+
+def test_version_and_geometry():
+    assert L.lib().fa_version() == 0x000100
+    bq, bk, threads, lds = L.geometry(128)
+    assert (bq, bk, threads) == (128, 64, 256)
+    assert lds == 2 * 2 * 64 * 128 * 2
+    with pytest.raises(L.FaArgumentError):
+        L.geometry(96)
+
+
+NULL = ctypes.c_void_p(0)
+
+
+def _status(fn, *args):
+    return getattr(L.lib(), fn)(*args)
+
+
+def test_invalid_arguments_rejected_before_any_launch():
+    lib = L.lib()
+    st = lib.fa_fwd_v1(NULL, NULL, NULL, NULL, 1, 1, 64, 128, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"null" in lib.fa_last_error()
+    st = lib.fa_fwd_v1(NULL, NULL, NULL, NULL, 0, 1, 64, 128, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"positive" in lib.fa_last_error()
+    st = lib.fa_fwd_v1(NULL, NULL, NULL, NULL, 1, 1, 64, 96, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED and b"d=96" in lib.fa_last_error()
+    st = lib.fa_fwd_v1(NULL, NULL, NULL, NULL, 1, 1, 64, 128, 7, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED
+    fake = ctypes.c_void_p(0x10000)
+    st = lib.fa_fwd_v1_tiled_d(fake, fake, fake, fake, 1, 1, 64, 128, 256, 32, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"d_tile" in lib.fa_last_error()
+    st = lib.fa_fwd_v1_tiled_d(fake, fake, fake, fake, 1, 1, 64, 128, 32, 0, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_INVALID_ARG
+    st = lib.fa_fwd_v1(ctypes.c_void_p(0x10002), fake, fake, fake, 1, 1, 64, 128, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"aligned" in lib.fa_last_error()
+
+
+def test_workspace_size_and_v2_checks():
+    lib = L.lib()
+    nbytes, ns = ctypes.c_size_t(), ctypes.c_int()
+    # C4: B32 H8 L4096 d128, KVTPB=4 -> 256-key splits -> 16 splits
+    assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, L.FA_DTYPE_BF16,
+                                        ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+    rows = 16 * 32 * 8 * 4096
+    assert ns.value == 16
+    assert nbytes.value == rows * 128 * 2 + rows * 4  # both parts already 256-aligned
+    assert nbytes.value > 2 ** 32  # 64-bit sizes (the reference overflows int32 here)
+    assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
+                                        ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+    assert ns.value == 2
+    assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 0, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
+                                        ctypes.byref(nbytes), None) == L.FA_ERR_INVALID_ARG
+    assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_BF16,
+                                        ctypes.byref(nbytes), None) == L.FA_ERR_UNSUPPORTED
+    fake = ctypes.c_void_p(0x10000)
+    st = lib.fa_fwd_v2(fake, fake, fake, fake, 1, 1, 100, 64, 32, 32, 1, fake, 16, L.FA_DTYPE_FP16,
+                       L.FA_DTYPE_FP32, NULL)
+    assert st == L.FA_ERR_WORKSPACE and b"workspace" in lib.fa_last_error()
+
+
+def test_partial_and_combine_checks():
+    lib = L.lib()
+    fake = ctypes.c_void_p(0x10000)
+    st = lib.fa_fwd_partial(fake, fake, fake, fake, fake, 1, 1, 100, 50, 64, 30, L.FA_DTYPE_BF16,
+                            L.FA_DTYPE_FP32, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"chunk_rows" in lib.fa_last_error()
+    st = lib.fa_combine(fake, fake, fake, 0, 1, 1, 100, 64, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
+    assert st == L.FA_ERR_INVALID_ARG
+
+
+def test_python_check_raises_typed_errors():
+    lib = L.lib()
+    with pytest.raises(L.FaArgumentError) as ei:
+        L.check(lib.fa_fwd_v1(NULL, NULL, NULL, NULL, 1, 1, 64, 64, L.FA_DTYPE_BF16, NULL))
+    assert isinstance(ei.value, ValueError) and ei.value.status == L.FA_ERR_INVALID_ARG
+
+
+def test_ops_reject_host_tensors():
+    import torch
+    from exploring_flash_attention_amd import ops
+    q = torch.zeros(1, 1, 64, 64, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.attention_v1(q, q, q)
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    monkeypatch.setattr(L, "_lib", None)
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        L.lib()
