@@ -1,0 +1,81 @@
+"""Multi-rank split-KV exchange on CPU: world_size 2 and 4 over gloo.
+
+The per-rank kernels need a GPU, so here dist._partial_fn / dist._combine_fn are replaced
+by the fp64 oracle (oracle.splitkv) computing the SAME layouts the HIP kernels write:
+o_part [W, B*H, L/W, d] (send layout: chunk j goes to rank j) and lse [W, B*H, L/W].
+What is under test is the product's exchange logic: chunking, the all_to_all_single
+pairing, the combine of the received partials and the final all_gather.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle.batched import attention_fp64
+from oracle.splitkv import combine_lse, partial_lse
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_partial(q, k, v, chunk_rows, partial_dtype):
+    B, H, Lq, d = q.shape
+    O, lse = partial_lse(q.double().numpy(), k.double().numpy(), v.double().numpy())
+    nch = Lq // chunk_rows
+    O = O.reshape(B * H, nch, chunk_rows, d).transpose(1, 0, 2, 3)
+    lse = lse.reshape(B * H, nch, chunk_rows).transpose(1, 0, 2)
+    return (torch.from_numpy(np.ascontiguousarray(O)).to(partial_dtype),
+            torch.from_numpy(np.ascontiguousarray(lse)).float())
+
+
+def _oracle_combine(o_part, lse, B, H, dtype):
+    S, BH, L, d = o_part.shape
+    O = combine_lse(o_part.double().numpy(), lse.double().numpy())
+    return torch.from_numpy(O.reshape(B, H, L, d)).to(dtype)
+
+
+def _worker(rank, world, port, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from exploring_flash_attention_amd import dist as fdist
+    fdist._partial_fn = _oracle_partial
+    fdist._combine_fn = _oracle_combine
+    g = torch.Generator().manual_seed(0)
+    B, H, L, d = 2, 3, 64, 32
+    q, k, v = (torch.randn(B, H, L, d, generator=g, dtype=torch.float64) for _ in range(3))
+    lo, hi = fdist.shard_bounds(L, world, rank)
+    local = fdist.splitkv_attention(q, k[:, :, lo:hi].contiguous(), v[:, :, lo:hi].contiguous(),
+                                    partial_dtype=torch.float64)
+    full = fdist.splitkv_attention(q, k[:, :, lo:hi].contiguous(), v[:, :, lo:hi].contiguous(),
+                                   partial_dtype=torch.float64, gather=True)
+    ref = attention_fp64(q.numpy(), k.numpy(), v.numpy())
+    err_local = np.abs(local.numpy() - ref[:, :, lo:hi]).max()
+    err_full = np.abs(full.numpy() - ref).max()
+    with open(f"{result_path}.{rank}", "w") as f:
+        f.write(f"{err_local} {err_full} {tuple(local.shape)} {tuple(full.shape)}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_splitkv_exchange_gloo(tmp_path, world):
+    port = _free_port()
+    path = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, port, path), nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        err_local, err_full, *_ = open(f"{path}.{r}").read().split(" ", 2)
+        assert float(err_local) < 1e-6 and float(err_full) < 1e-6  # fp32 lse, as on the GPU
+
+
+def test_shard_bounds():
+    from exploring_flash_attention_amd.dist import shard_bounds
+    assert [shard_bounds(16384, 8, r) for r in (0, 7)] == [(0, 2048), (14336, 16384)]
+    with pytest.raises(ValueError):
+        shard_bounds(100, 8, 0)
