@@ -52,21 +52,18 @@ template <> struct Mma<_Float16> {
     }
 };
 
-// XOR swizzle of the 16-byte chunk index inside one LDS row of D 16-bit elements.
-// Chosen so that (a) the ds_read_b128 row reads of the 32x32x16 A operand (16 distinct
-// rows per lane group, one chunk) and (b) the ds_read_b64_tr_b16 transposed reads
-// (4 consecutive rows x 32 columns per 32-lane half) both hit 16 distinct 16-byte bank
-// slots, i.e. are conflict-free.  DESIGN.md section "LDS image" has the proof sketch.
-template <int D>
-__device__ __forceinline__ int swz(int row) {
-    if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
-    else if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
-    else return (row >> 2) & 3;  // D == 32
-}
-
+// LDS image of one [kBK][D] K or V tile: 8-row x 4-chunk (8 x 32 columns, 512 B)
+// subtiles, subtile (row>>3, ch>>2) at (row>>3)*8*ROWB + 512*(ch>>2), and inside it row
+// (row&7) at 64 B strides with the 16-byte chunk XOR-swizzled by (row>>2)&3.
+// Bank analysis ("LDS image"): the ds_read_b128 row reads of the 32x32x16 A
+// operand (16 distinct rows per lane group, one chunk) and the ds_read_b64_tr_b16
+// transposed reads (4 consecutive rows x 4 chunks per 32-lane half) both touch 16
+// distinct 16-byte bank slots -- conflict-free -- and both need only two base
+// addresses per lane (every other read is base + an immediate).
 template <int D>
 __device__ __forceinline__ int lds_off(int row, int chunk) {
-    return row * (D * 2) + 16 * (chunk ^ swz<D>(row));
+    return (row >> 3) * (8 * D * 2) + 512 * (chunk >> 2) + 64 * (row & 7) +
+           16 * ((chunk & 3) ^ ((row >> 2) & 3));
 }
 
 // Bijective workgroup remap: blocks b and b+8 share an XCD (observed round-robin
@@ -86,11 +83,23 @@ __device__ __forceinline__ float pair_sum(float x) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+template <typename T> struct Pack;
+template <> struct Pack<__bf16> { typedef __bf16 v2 __attribute__((ext_vector_type(2))); };
+template <> struct Pack<_Float16> { typedef _Float16 v2 __attribute__((ext_vector_type(2))); };
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> one dword of two 16-bit values (one v_cvt_pk_{bf16,f16}_f32, RNE)
 template <typename T>
 __device__ __forceinline__ unsigned pack2(float a, float b) {
-    T x = static_cast<T>(a), y = static_cast<T>(b);
-    return (unsigned)__builtin_bit_cast(unsigned short, x) |
-           ((unsigned)__builtin_bit_cast(unsigned short, y) << 16);
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a, b}, typename Pack<T>::v2));
+}
+
+// Buffer resource over [base, base + bytes): loads past the end return 0 (the hardware
+// range check does the tail clamping, no per-lane address arithmetic in the KV loop).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                             (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff),
+                                             0x00020000);
 }
 
 template <typename T, typename PT, int D, bool PARTIAL>
@@ -103,6 +112,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     constexpr int CPT = kBK * NCH / kThreads; // staged chunks per thread per tile
     constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
     constexpr int NDB = D / 32;               // 32-column blocks of O
+    // Deferred rescale (defer-max): the running max m is only moved when some row's tile
+    // max exceeds it by more than kThr (log2 units), so most tiles skip the O *= alpha
+    // pass; P is then bounded by 2^kThr instead of 1, well inside fp32/bf16 range.
+    constexpr float kThr = 4.f;  // 8 costs accuracy on peaked rows (see tests)
     static_assert(kBK * NCH % kThreads == 0, "tile must split evenly over threads");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -123,32 +136,37 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
     const int ntiles = (int)((kv_end - kv_begin + kBK - 1) / kBK);
 
+    // Buffer descriptors: K/V cover exactly this split's keys, so the staging loads of the
+    // last (partial) tile read zeros past kv_end with no clamping code.
     const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D;
-    const unsigned short* Kh = (const unsigned short*)a.k + bh * a.Lk * D;
-    const unsigned short* Vh = (const unsigned short*)a.v + bh * a.Lk * D;
+    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, a.Lq * ROWB);
+    const __amdgpu_buffer_rsrc_t krs =
+        make_rsrc((const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D, (kv_end - kv_begin) * ROWB);
+    const __amdgpu_buffer_rsrc_t vrs =
+        make_rsrc((const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D, (kv_end - kv_begin) * ROWB);
 
-    // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7].
+    // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7].  Rows past Lq
+    // read zeros and are never stored.
     const int64_t q_row = (int64_t)qt * kBQ + wid * kRowsPerWave + l32;
-    const int64_t q_row_c = q_row < a.Lq ? q_row : a.Lq - 1;
     v8 qf[NKS];
+    {
+        const int qoff = (int)(q_row * ROWB) + hf * 16;
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-        u32x4 raw = *(const u32x4*)(Qh + q_row_c * D + ks * 16 + hf * 8);
-        qf[ks] = __builtin_bit_cast(v8, raw);
+        for (int ks = 0; ks < NKS; ++ks)
+            qf[ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, qoff + ks * 32, 0, 0));
     }
 
     // Register staging of the K and V tiles: thread t moves 16-byte chunks
-    // t, t + kThreads, ... of the [kBK][D] tile (coalesced global reads).
+    // t, t + kThreads, ... of the [kBK][D] tile (coalesced); per-lane offsets are fixed,
+    // the tile offset is a scalar.
     u32x4 kst[CPT], vst[CPT];
-    auto stage_load = [&](int64_t kv0) {
+    auto stage_load = [&](int t) {
+        const int soff = t * TILEB;
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const int idx = tid + i * kThreads;
-            const int row = idx / NCH, ch = idx % NCH;
-            int64_t g = kv0 + row;
-            g = g < kv_end ? g : kv_end - 1;  // clamp: padded keys are masked to -inf
-            kst[i] = *(const u32x4*)(Kh + g * D + ch * 8);
-            vst[i] = *(const u32x4*)(Vh + g * D + ch * 8);
+            const int g = (tid + i * kThreads) * 16;
+            kst[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, g, soff, 0);
+            vst[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, g, soff, 0);
         }
     };
     auto stage_write = [&](int buf) {
@@ -157,8 +175,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int idx = tid + i * kThreads;
-            const int row = idx / NCH, ch = idx % NCH;
-            const int off = lds_off<D>(row, ch);
+            const int off = lds_off<D>(idx / NCH, idx % NCH);
             *(u32x4*)(kb + off) = kst[i];
             *(u32x4*)(vb + off) = vst[i];
         }
@@ -167,7 +184,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     f32x16 o[NDB];
 #pragma unroll
     for (int db = 0; db < NDB; ++db) o[db] = f32x16{};
-    float m = -INFINITY;  // running max, in units of log2 (scores * scale_log2)
+    float m = -INFINITY;  // reference max of the row, in log2 units (scores * scale_log2)
     float l = 0.f;        // this lane's half of the running denominator
     const float c = a.scale_log2;
 
@@ -176,14 +193,19 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     const int tr_row = 4 * (grp >> 1) + (gi >> 2);
     const int tr_col = 16 * (grp & 1) + 4 * (gi & 3);
 
-    stage_load(kv_begin);
+    stage_load(0);
     stage_write(0);
+    // Make the Q fragments' loads retire here: otherwise hipcc's waitcnt pass carries them
+    // as pending into the loop header and, merging that state with the back edge, puts
+    // vmcnt(7..0) waits in front of every QK^T MFMA -- draining the next tile's prefetch
+    // on every iteration.
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
     __syncthreads();
 
     for (int t = 0; t < ntiles; ++t) {
-        const int64_t kv0 = kv_begin + (int64_t)t * kBK;
         const bool has_next = t + 1 < ntiles;
-        if (has_next) stage_load(kv0 + kBK);
+        if (has_next) stage_load(t + 1);
         const char* kb = smem + (t & 1) * 2 * TILEB;
         const char* vb = kb + TILEB;
 
@@ -192,17 +214,16 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int b2 = 0; b2 < 2; ++b2) {
             s[b2] = f32x16{};
-            const int row = b2 * 32 + l32;
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                const v8 kf = *(const v8*)(kb + lds_off<D>(row, 2 * ks + hf));
+                const v8 kf = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * ks + hf));
                 s[b2] = M::mma(kf, qf[ks], s[b2]);
             }
         }
 
         // mask keys past the end of this split (only the last, partial tile)
-        if (kv_end - kv0 < kBK) {
-            const int valid = (int)(kv_end - kv0);
+        const int valid = (int)(kv_end - kv_begin) - t * kBK;
+        if (valid < kBK) {
 #pragma unroll
             for (int b2 = 0; b2 < 2; ++b2)
 #pragma unroll
@@ -212,28 +233,36 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
                 }
         }
 
-        float mx = s[0][0];
+        // row max: 4 independent chains, then the lane pair (l, l+32)
+        float mx4[4];
 #pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
+        for (int j = 0; j < 4; ++j) mx4[j] = fmaxf(s[j >> 1][8 * (j & 1)], s[j >> 1][8 * (j & 1) + 1]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
-        mx = pair_max(mx);
-        const float m_new = fmaxf(m, mx * c);
-        const float alpha = __builtin_amdgcn_exp2f(m - m_new);
-        m = m_new;
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 2; r < 8; ++r) mx4[j] = fmaxf(mx4[j], s[j >> 1][8 * (j & 1) + r]);
+        const float mx = pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
 
-        float sum = 0.f;
+        // deferred rescale: wave-uniform decision, taken before any P of this tile exists
+        if (__builtin_amdgcn_ballot_w64(mx > m + kThr)) {
+            const float m_new = fmaxf(m, mx);
+            const float alpha = __builtin_amdgcn_exp2f(m - m_new);
+            m = m_new;
+            l *= alpha;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+        }
+
+        float sum4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b2 = 0; b2 < 2; ++b2)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[b2][r], c, -m_new));
+                const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[b2][r], c, -m));
                 s[b2][r] = p;
-                sum += p;
+                sum4[(b2 * 16 + r) & 3] += p;
             }
-        l = l * alpha + sum;
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+        l += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
 
         // P^T packed to 16-bit: registers 8*ss .. 8*ss+7 of block b2 form the B operand
         // of k-step ss; its element j is key 16*ss + 8*(j>>2) + 4*hf + (j&3) of the block.
@@ -243,15 +272,14 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 u32x4 u;
-                u[0] = pack2<T>(s[b2][8 * ss + 0], s[b2][8 * ss + 1]);
-                u[1] = pack2<T>(s[b2][8 * ss + 2], s[b2][8 * ss + 3]);
-                u[2] = pack2<T>(s[b2][8 * ss + 4], s[b2][8 * ss + 5]);
-                u[3] = pack2<T>(s[b2][8 * ss + 6], s[b2][8 * ss + 7]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) u[j] = pack2<T>(s[b2][8 * ss + 2 * j], s[b2][8 * ss + 2 * j + 1]);
                 pb[b2][ss] = __builtin_bit_cast(v8, u);
             }
 
         // O^T[dv][q] += V^T[dv][key] . P^T[key][q]; the A operand's element j must be
         // the same key as pb's element j: two transposed reads of 4 keys each.
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
 #pragma unroll
@@ -261,7 +289,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
                     const int row = b2 * 32 + 16 * ss + tr_row;
                     const int col = db * 32 + tr_col;
                     const int sub = (col & 7) * 2;  // 0 or 8 bytes inside the chunk
-                    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
                     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (lds_s16x4*)(vb + lds_off<D>(row, col >> 3) + sub));
                     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -310,6 +337,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
                     *(u32x2*)((unsigned short*)Op + col) = u;
                 }
             }
+        // lse in log2 units: m + log2(l)  (v_log_f32 is log2)
         if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m + __builtin_amdgcn_logf(l_tot);
     }
 }
