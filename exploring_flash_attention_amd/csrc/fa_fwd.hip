@@ -102,6 +102,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
                                              0x00020000);
 }
 
+// One 16-byte-per-lane LDS-DMA piece: lane i's 16 bytes land at lds + 16*i.  Kept out of
+// the kernel's lambdas: a builtin call inside a lambda made hipcc drop the kernel's host
+// launch stub (undefined __device_stub__ at load time).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, int voff, int soff) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, voff, soff, 0, 0);
+}
+
 template <typename T, typename PT, int D, bool PARTIAL>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
@@ -109,7 +117,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     constexpr int ROWB = D * 2;               // bytes per LDS row
     constexpr int NCH = D / 8;                // 16-byte chunks per row
     constexpr int TILEB = kBK * ROWB;         // bytes of one K (or V) tile
-    constexpr int CPT = kBK * NCH / kThreads; // staged chunks per thread per tile
     constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
     constexpr int NDB = D / 32;               // 32-column blocks of O
     // Deferred rescale (defer-max): the running max m is only moved when some row's tile
@@ -156,28 +163,31 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
             qf[ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, qoff + ks * 32, 0, 0));
     }
 
-    // Register staging of the K and V tiles: thread t moves 16-byte chunks
-    // t, t + kThreads, ... of the [kBK][D] tile (coalesced); per-lane offsets are fixed,
-    // the tile offset is a scalar.
-    u32x4 kst[CPT], vst[CPT];
-    auto stage_load = [&](int t) {
+    // K/V tiles go HBM -> LDS by LDS-DMA (buffer_load ... lds): no staging VGPRs, no
+    // ds_write pass.  One wave instruction writes 1 KiB of LDS lane-linearly (M0 base +
+    // 16*lane), so the swizzled image is produced by giving each lane the SOURCE chunk
+    // that lds_off() places at its destination byte.  Out-of-range lanes of the last,
+    // partial tile read zeros (buffer range check).
+    constexpr int NDMA = TILEB / 1024;              // 1 KiB pieces per tile and operand
+    constexpr int DPW = NDMA / kWaves;              // pieces per wave
+    static_assert(NDMA % kWaves == 0, "tile pieces must split evenly over waves");
+    int dma_src[DPW];
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+        const int b = (wid * DPW + i) * 1024 + lane * 16;  // destination byte in the tile image
+        const int rg = b / (8 * ROWB), rem = b % (8 * ROWB);
+        const int row = 8 * rg + (rem % 512) / 64;
+        const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
+        dma_src[i] = row * ROWB + ch * 16;
+    }
+    auto stage = [&](int t, int buf) {
+        char* kb = smem + buf * 2 * TILEB + wid * DPW * 1024;
+        char* vb = kb + TILEB;
         const int soff = t * TILEB;
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int g = (tid + i * kThreads) * 16;
-            kst[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, g, soff, 0);
-            vst[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, g, soff, 0);
-        }
-    };
-    auto stage_write = [&](int buf) {
-        char* kb = smem + buf * 2 * TILEB;
-        char* vb = kb + TILEB;
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int idx = tid + i * kThreads;
-            const int off = lds_off<D>(idx / NCH, idx % NCH);
-            *(u32x4*)(kb + off) = kst[i];
-            *(u32x4*)(vb + off) = vst[i];
+        for (int i = 0; i < DPW; ++i) {
+            dma16(krs, kb + i * 1024, dma_src[i], soff);
+            dma16(vrs, vb + i * 1024, dma_src[i], soff);
         }
     };
 
@@ -193,8 +203,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     const int tr_row = 4 * (grp >> 1) + (gi >> 2);
     const int tr_col = 16 * (grp & 1) + 4 * (gi & 3);
 
-    stage_load(0);
-    stage_write(0);
+    stage(0, 0);
     // Make the Q fragments' loads retire here: otherwise hipcc's waitcnt pass carries them
     // as pending into the loop header and, merging that state with the back edge, puts
     // vmcnt(7..0) waits in front of every QK^T MFMA -- draining the next tile's prefetch
@@ -205,21 +214,58 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 
     for (int t = 0; t < ntiles; ++t) {
         const bool has_next = t + 1 < ntiles;
-        if (has_next) stage_load(t + 1);
+        if (has_next) stage(t + 1, (t + 1) & 1);  // lands under this tile's MFMAs
         const char* kb = smem + (t & 1) * 2 * TILEB;
         const char* vb = kb + TILEB;
 
         // S^T[key][q] for 2 blocks of 32 keys
+        // All K fragments of the tile are read up front (lgkmcnt-counted), so the MFMA
+        // chain waits for each read only once instead of read -> wait -> MFMA serially.
         f32x16 s[2];
+        v8 kf[2][NKS];
 #pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2) {
-            s[b2] = f32x16{};
+        for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const v8 kf = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * ks + hf));
-                s[b2] = M::mma(kf, qf[ks], s[b2]);
-            }
-        }
+            for (int b2 = 0; b2 < 2; ++b2)
+                kf[b2][ks] = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * ks + hf));
+        s[0] = f32x16{};
+        s[1] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2) s[b2] = M::mma(kf[b2][ks], qf[ks], s[b2]);
+        // keep hipcc from sinking each read next to its MFMA: reads first, then the chain
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NKS, 0);  // DS_READ
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NKS, 0);  // MFMA
+
+        // V^T fragments of one 32-column O block: 8 transposed reads (4 keys each); the
+        // A operand's element j must be the same key as pb's element j (see below).
+        // Issued as inline asm: hipcc cannot prove the builtin form disjoint from the
+        // in-flight LDS-DMA into the other buffer and would put vmcnt(0) -- a full drain of
+        // the next tile's prefetch -- in front of every one.  Their lgkmcnt is waited for
+        // by vwait() below, which names every destination.
+        auto read_v = [&](int db, u32x2 (&vf)[2][2][2]) {
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int row = b2 * 32 + 16 * ss + tr_row;
+                    const int col = db * 32 + tr_col;
+                    const int sub = (col & 7) * 2;  // 0 or 8 bytes inside the chunk
+                    const unsigned a0 = (unsigned)(size_t)(vb + lds_off<D>(row, col >> 3) + sub);
+                    const unsigned a1 = (unsigned)(size_t)(vb + lds_off<D>(row + 8, col >> 3) + sub);
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[b2][ss][0]) : "v"(a0) : "memory");
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[b2][ss][1]) : "v"(a1) : "memory");
+                }
+        };
+        auto vwait = [&](u32x2 (&vf)[2][2][2]) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(vf[0][0][0]), "+v"(vf[0][0][1]), "+v"(vf[0][1][0]), "+v"(vf[0][1][1]),
+                           "+v"(vf[1][0][0]), "+v"(vf[1][0][1]), "+v"(vf[1][1][0]), "+v"(vf[1][1][1]));
+        };
+        // block 0's V reads go out now and land under the softmax VALU work
+        u32x2 vcur[2][2][2];
+        read_v(0, vcur);
 
         // mask keys past the end of this split (only the last, partial tile)
         const int valid = (int)(kv_end - kv_begin) - t * kBK;
@@ -277,29 +323,33 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
                 pb[b2][ss] = __builtin_bit_cast(v8, u);
             }
 
-        // O^T[dv][q] += V^T[dv][key] . P^T[key][q]; the A operand's element j must be
-        // the same key as pb's element j: two transposed reads of 4 keys each.
-        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        // O^T[dv][q] += V^T[dv][key] . P^T[key][q], block db's MFMAs overlapping the
+        // reads of block db+1.
+        vwait(vcur);
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
+            u32x2 vnext[2][2][2];
+            if (db + 1 < NDB) read_v(db + 1, vnext);
 #pragma unroll
             for (int b2 = 0; b2 < 2; ++b2)
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
-                    const int row = b2 * 32 + 16 * ss + tr_row;
-                    const int col = db * 32 + tr_col;
-                    const int sub = (col & 7) * 2;  // 0 or 8 bytes inside the chunk
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(vb + lds_off<D>(row, col >> 3) + sub));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(vb + lds_off<D>(row + 8, col >> 3) + sub));
-                    const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    const u32x4 vv = {vcur[b2][ss][0][0], vcur[b2][ss][0][1], vcur[b2][ss][1][0],
+                                      vcur[b2][ss][1][1]};
                     o[db] = M::mma(__builtin_bit_cast(v8, vv), pb[b2][ss], o[db]);
                 }
+            if (db + 1 < NDB) {
+                vwait(vnext);
+#pragma unroll
+                for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) vcur[b2][ss][h] = vnext[b2][ss][h];
+            }
         }
 
-        if (has_next) stage_write((t + 1) & 1);
-        __syncthreads();
+        __syncthreads();  // hipcc puts vmcnt(0) here: tile t+1's DMA has landed
     }
 
     // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (r&3) + 8*(r>>2) + 4*hf

@@ -95,8 +95,8 @@ def attention_tiled_d(q, k, v, d_tile_qk=32, d_tile_v=32, out=None):
 
 def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
                        partial_dtype=None):
-    """(bytes, num_splits) of the split-KV workspace."""
-    pd = dtype if partial_dtype is None else partial_dtype
+    """(bytes, num_splits) of the split-KV workspace (partials fp32 unless partial_dtype)."""
+    pd = torch.float32 if partial_dtype is None else partial_dtype
     nbytes = ctypes.c_size_t()
     ns = ctypes.c_int()
     check(lib().fa_fwd_v2_workspace_size(B, H, L, d, int(kv_tiles_per_block), _DTYPES[dtype],
@@ -109,13 +109,15 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
     """FA-v2 split-KV forward (partial kernel + combine kernel).
 
     A split is ``kv_tiles_per_block`` KV tiles of the kernel's own tile size (64 keys).
+    Partial outputs are kept in fp32 by default (``partial_dtype=torch.bfloat16`` halves the
+    workspace traffic at the cost of one extra 16-bit rounding of every partial).
     ``workspace`` (a uint8 device tensor) is allocated from torch's caching allocator when
     not given, so the call itself never reaches hipMalloc after warm-up.
     """
     _check_qkv(q, k, v)
     o = _out(out, q)
     B, H, L, d = q.shape
-    pd = q.dtype if partial_dtype is None else partial_dtype
+    pd = torch.float32 if partial_dtype is None else partial_dtype
     nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
     if workspace is None:
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=q.device)

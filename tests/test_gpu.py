@@ -125,14 +125,14 @@ def _variants():
         "v1": ops.attention_v1,
         "tiled_d": lambda q, k, v: ops.attention_tiled_d(q, k, v, 16, 32),
         "v2_kvtpb1_f32": lambda q, k, v: ops.attention_v2(q, k, v, 1, partial_dtype=torch.float32),
-        "v2_kvtpb4": lambda q, k, v: ops.attention_v2(q, k, v, 4),
+        "v2_kvtpb4_bf16": lambda q, k, v: ops.attention_v2(q, k, v, 4, partial_dtype=torch.bfloat16),
     }
 
 
 SHAPES = [(1, 1, 1), (1, 2, 65), (2, 3, 200), (1, 2, 512)]
 
 
-@pytest.mark.parametrize("variant", ["v1", "tiled_d", "v2_kvtpb1_f32", "v2_kvtpb4"])
+@pytest.mark.parametrize("variant", ["v1", "tiled_d", "v2_kvtpb1_f32", "v2_kvtpb4_bf16"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
 @pytest.mark.parametrize("d", [32, 64, 128])
 def test_matrix(gpu, variant, dtype, d):
@@ -164,11 +164,15 @@ def test_running_max_rescale_is_exercised(gpu):
     v = torch.randn(B, H, L, d, generator=g)
     k[0, 0, -1] = q[0, 0, 0] * 2  # one very large score in the last tile for query 0
     q, k, v = (x.to(torch.bfloat16) for x in (q, k, v))
-    for fn in _variants().values():
+    ref = _ref(q, k, v)
+    for name, fn in _variants().items():
         out = fn(q.to(gpu), k.to(gpu), v.to(gpu)).float().cpu().numpy()
-        # scores x3 sharpen the softmax and grow |O|; the hard gate (1e-2) applies
-        m = check_accuracy(out, _ref(q, k, v), max_rel_tol=float("inf"))
-        assert m["mean_rel"] <= 1e-2, m
+        m = accuracy_metrics(out, ref)
+        # scores x3 sharpen the softmax and grow |O|: the hard gate (1e-2) applies, except
+        # that bf16 split-KV partials add one more 16-bit rounding of the dominant partial
+        # (1.37e-2 here, reproduced exactly by a NumPy emulation of the kernel's rounding)
+        limit = 2e-2 if name.endswith("bf16") else 1e-2
+        assert m["max_abs"] <= limit and m["mean_rel"] <= 1e-2, (name, m)
 
 
 # ----------------------------------------------------------------------------------------
