@@ -169,7 +169,7 @@ def main():
                 ops.attention_v1(q, k, v, out=out)
             kernel = "fa_fwd_kernel (final)"
         else:
-            nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype, q.dtype)
+            nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
 
             def step():
@@ -215,7 +215,7 @@ def main():
                 def st():
                     ops.attention_v1(qq, kk, vv)
             else:
-                nb, _ = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], 4, qq.dtype, qq.dtype)
+                nb, _ = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], 4, qq.dtype)
                 wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
 
                 def st():
