@@ -27,7 +27,31 @@
 //     that is bank-conflict-free for both the row reads and the transposed reads.
 //   * blockIdx is remapped so that all query tiles of one (b,h) land on one XCD and
 //     share that head's K/V in the XCD's L2.
+#include <utility>
+
 #include "fa_internal.hpp"
+
+// Build knobs for A/B experiments (scripts/build_variants.sh, scripts/ab.py); the
+// defaults are the measured-best settings.  FA_ABL_* are ablations (wrong results,
+// timing only) used to attribute time to the kernel's phases.
+#ifndef FA_QK_SCHED
+#define FA_QK_SCHED 0
+#endif
+#ifndef FA_ABL_NOEXP
+#define FA_ABL_NOEXP 0
+#endif
+#ifndef FA_ABL_NODMA
+#define FA_ABL_NODMA 0
+#endif
+#ifndef FA_ABL_NOPV
+#define FA_ABL_NOPV 0
+#endif
+#ifndef FA_ABL_NOQK
+#define FA_ABL_NOQK 0
+#endif
+#ifndef FA_QK_LEAD
+#define FA_QK_LEAD 4
+#endif
 
 namespace fa {
 
@@ -102,6 +126,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
                                              0x00020000);
 }
 
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N), so that each
+// body can feed i into an inline-asm "i" (immediate) operand.
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // One 16-byte-per-lane LDS-DMA piece: lane i's 16 bytes land at lds + 16*i.  Kept out of
 // the kernel's lambdas: a builtin call inside a lambda made hipcc drop the kernel's host
 // launch stub (undefined __device_stub__ at load time).
@@ -115,17 +150,19 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     constexpr int ROWB = D * 2;               // bytes per LDS row
-    constexpr int NCH = D / 8;                // 16-byte chunks per row
     constexpr int TILEB = kBK * ROWB;         // bytes of one K (or V) tile
     constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
     constexpr int NDB = D / 32;               // 32-column blocks of O
-    // Deferred rescale (defer-max): the running max m is only moved when some row's tile
-    // max exceeds it by more than kThr (log2 units), so most tiles skip the O *= alpha
-    // pass; P is then bounded by 2^kThr instead of 1, well inside fp32/bf16 range.
-    constexpr float kThr = 4.f;  // 8 costs accuracy on peaked rows (see tests)
-    static_assert(kBK * NCH % kThreads == 0, "tile must split evenly over threads");
+    // Deferred rescale (defer-max): the reference max m of a row is only moved when some
+    // row of the wave sees a tile max above m + kThr (log2 units); P is then bounded by
+    // 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows (the
+    // dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
+    constexpr float kThr = 4.f;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // LDS: K ring (2 slots) then V ring (2 slots), one [kBK][D] tile image per slot.
+    char* const kring = smem;
+    char* const vring = smem + 2 * TILEB;
 
     const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int qt = w % a.nqt;
@@ -141,16 +178,17 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 
     const int64_t kv_begin = (int64_t)split * a.kv_per_split;
     const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
-    const int ntiles = (int)((kv_end - kv_begin + kBK - 1) / kBK);
+    const int nkv = (int)(kv_end - kv_begin);
+    const int ntiles = (nkv + kBK - 1) / kBK;
 
-    // Buffer descriptors: K/V cover exactly this split's keys, so the staging loads of the
-    // last (partial) tile read zeros past kv_end with no clamping code.
+    // Buffer descriptors: K/V cover exactly this split's keys, so the DMA of the last
+    // (partial) tile reads zeros past kv_end with no clamping code.
     const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D;
     const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, a.Lq * ROWB);
     const __amdgpu_buffer_rsrc_t krs =
-        make_rsrc((const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D, (kv_end - kv_begin) * ROWB);
+        make_rsrc((const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D, (int64_t)nkv * ROWB);
     const __amdgpu_buffer_rsrc_t vrs =
-        make_rsrc((const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D, (kv_end - kv_begin) * ROWB);
+        make_rsrc((const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D, (int64_t)nkv * ROWB);
 
     // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7].  Rows past Lq
     // read zeros and are never stored.
@@ -166,11 +204,11 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     // K/V tiles go HBM -> LDS by LDS-DMA (buffer_load ... lds): no staging VGPRs, no
     // ds_write pass.  One wave instruction writes 1 KiB of LDS lane-linearly (M0 base +
     // 16*lane), so the swizzled image is produced by giving each lane the SOURCE chunk
-    // that lds_off() places at its destination byte.  Out-of-range lanes of the last,
-    // partial tile read zeros (buffer range check).
-    constexpr int NDMA = TILEB / 1024;              // 1 KiB pieces per tile and operand
-    constexpr int DPW = NDMA / kWaves;              // pieces per wave
-    static_assert(NDMA % kWaves == 0, "tile pieces must split evenly over waves");
+    // that lds_off() places at its destination byte.
+    constexpr int NDMA = TILEB / 1024;                      // 1 KiB pieces per tile
+    constexpr int DPW = NDMA >= kWaves ? NDMA / kWaves : 1;  // pieces per (active) wave
+    static_assert(NDMA % kWaves == 0 || kWaves % NDMA == 0, "tile pieces must split over waves");
+    const bool dma_wave = wid * DPW < NDMA;                  // waves past the last piece idle
     int dma_src[DPW];
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
@@ -180,95 +218,75 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
         const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
         dma_src[i] = row * ROWB + ch * 16;
     }
-    auto stage = [&](int t, int buf) {
-        char* kb = smem + buf * 2 * TILEB + wid * DPW * 1024;
-        char* vb = kb + TILEB;
-        const int soff = t * TILEB;
+    auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, char* slot, int t) {
+        if (NDMA >= kWaves || dma_wave) {
 #pragma unroll
-        for (int i = 0; i < DPW; ++i) {
-            dma16(krs, kb + i * 1024, dma_src[i], soff);
-            dma16(vrs, vb + i * 1024, dma_src[i], soff);
+            for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], t * TILEB);
         }
     };
-
-    f32x16 o[NDB];
-#pragma unroll
-    for (int db = 0; db < NDB; ++db) o[db] = f32x16{};
-    float m = -INFINITY;  // reference max of the row, in log2 units (scores * scale_log2)
-    float l = 0.f;        // this lane's half of the running denominator
-    const float c = a.scale_log2;
 
     // transposed-read geometry (constant per lane)
     const int grp = lane >> 4, gi = lane & 15;
     const int tr_row = 4 * (grp >> 1) + (gi >> 2);
     const int tr_col = 16 * (grp & 1) + 4 * (gi & 3);
 
-    stage(0, 0);
-    // Make the Q fragments' loads retire here: otherwise hipcc's waitcnt pass carries them
-    // as pending into the loop header and, merging that state with the back edge, puts
-    // vmcnt(7..0) waits in front of every QK^T MFMA -- draining the next tile's prefetch
-    // on every iteration.
+    f32x16 o[NDB];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
-    __syncthreads();
+    for (int db = 0; db < NDB; ++db) o[db] = f32x16{};
+    float m = -INFINITY;  // reference max of the row, log2 units (scores * scale_log2)
+    float l = 0.f;        // this lane's half of the running denominator
+    const float c = a.scale_log2;
 
-    for (int t = 0; t < ntiles; ++t) {
-        const bool has_next = t + 1 < ntiles;
-        if (has_next) stage(t + 1, (t + 1) & 1);  // lands under this tile's MFMAs
-        const char* kb = smem + (t & 1) * 2 * TILEB;
-        const char* vb = kb + TILEB;
-
-        // S^T[key][q] for 2 blocks of 32 keys
-        // All K fragments of the tile are read up front (lgkmcnt-counted), so the MFMA
-        // chain waits for each read only once instead of read -> wait -> MFMA serially.
-        f32x16 s[2];
-        v8 kf[2][NKS];
+    // S^T[key][q] = K . Q^T for one tile (two 32-key blocks).  K fragments are read in
+    // groups of two k-steps, one group ahead of the MFMAs that consume it.
+    auto qk = [&](const char* kb, f32x16 (&s)[2]) {
+        constexpr int G = 2;  // k-steps per read group
+        v8 kf[2][2][G];       // [buffer][b2][k-step in group]
+        auto rd = [&](int g, v8 (&dst)[2][G]) {
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
+            for (int j = 0; j < G; ++j)
 #pragma unroll
-            for (int b2 = 0; b2 < 2; ++b2)
-                kf[b2][ks] = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * ks + hf));
+                for (int b2 = 0; b2 < 2; ++b2)
+                    dst[b2][j] = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * (g * G + j) + hf));
+        };
         s[0] = f32x16{};
         s[1] = f32x16{};
+        rd(0, kf[0]);
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
+        for (int g = 0; g < NKS / G; ++g) {
+            if (g + 1 < NKS / G) rd(g + 1, kf[(g + 1) & 1]);
 #pragma unroll
-            for (int b2 = 0; b2 < 2; ++b2) s[b2] = M::mma(kf[b2][ks], qf[ks], s[b2]);
-        // keep hipcc from sinking each read next to its MFMA: reads first, then the chain
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NKS, 0);  // DS_READ
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NKS, 0);  // MFMA
-
-        // V^T fragments of one 32-column O block: 8 transposed reads (4 keys each); the
-        // A operand's element j must be the same key as pb's element j (see below).
-        // Issued as inline asm: hipcc cannot prove the builtin form disjoint from the
-        // in-flight LDS-DMA into the other buffer and would put vmcnt(0) -- a full drain of
-        // the next tile's prefetch -- in front of every one.  Their lgkmcnt is waited for
-        // by vwait() below, which names every destination.
-        auto read_v = [&](int db, u32x2 (&vf)[2][2][2]) {
+            for (int j = 0; j < G; ++j)
 #pragma unroll
-            for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    const int row = b2 * 32 + 16 * ss + tr_row;
-                    const int col = db * 32 + tr_col;
-                    const int sub = (col & 7) * 2;  // 0 or 8 bytes inside the chunk
-                    const unsigned a0 = (unsigned)(size_t)(vb + lds_off<D>(row, col >> 3) + sub);
-                    const unsigned a1 = (unsigned)(size_t)(vb + lds_off<D>(row + 8, col >> 3) + sub);
-                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[b2][ss][0]) : "v"(a0) : "memory");
-                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[b2][ss][1]) : "v"(a1) : "memory");
+                for (int b2 = 0; b2 < 2; ++b2) {
+#if FA_ABL_NOQK
+                    asm volatile("" ::"v"(kf[g & 1][b2][j]));
+                    s[b2][j] += (float)qf[g * G + j][0];
+#else
+                    s[b2] = M::mma(kf[g & 1][b2][j], qf[g * G + j], s[b2]);
+#endif
                 }
-        };
-        auto vwait = [&](u32x2 (&vf)[2][2][2]) {
-            asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(vf[0][0][0]), "+v"(vf[0][0][1]), "+v"(vf[0][1][0]), "+v"(vf[0][1][1]),
-                           "+v"(vf[1][0][0]), "+v"(vf[1][0][1]), "+v"(vf[1][1][0]), "+v"(vf[1][1][1]));
-        };
-        // block 0's V reads go out now and land under the softmax VALU work
-        u32x2 vcur[2][2][2];
-        read_v(0, vcur);
-
-        // mask keys past the end of this split (only the last, partial tile)
-        const int valid = (int)(kv_end - kv_begin) - t * kBK;
+        }
+    };
+    // P = 2^(S*c - m) in place, and its row sum into l
+    auto exp_tile = [&](f32x16 (&s)[2]) {
+        float sum4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+#if FA_ABL_NOEXP
+                s[b2][r] = __builtin_fmaf(s[b2][r], c, -m);
+#else
+                s[b2][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[b2][r], c, -m));
+#endif
+                sum4[(b2 * 16 + r) & 3] += s[b2][r];
+            }
+        l += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
+    };
+    // keys past the end of the split (only in the last, partial tile) -> -inf
+    auto mask = [&](int t, f32x16 (&s)[2]) {
+        const int valid = nkv - t * kBK;
         if (valid < kBK) {
 #pragma unroll
             for (int b2 = 0; b2 < 2; ++b2)
@@ -278,8 +296,9 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
                     if (key >= valid) s[b2][r] = -INFINITY;
                 }
         }
-
-        // row max: 4 independent chains, then the lane pair (l, l+32)
+    };
+    // row max of a (masked) tile, both lane halves, in log2 units
+    auto rowmax = [&](const f32x16 (&s)[2]) {
         float mx4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) mx4[j] = fmaxf(s[j >> 1][8 * (j & 1)], s[j >> 1][8 * (j & 1) + 1]);
@@ -287,9 +306,44 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int r = 2; r < 8; ++r) mx4[j] = fmaxf(mx4[j], s[j >> 1][8 * (j & 1) + r]);
-        const float mx = pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
+        return pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
+    };
+    // V^T fragments of (32-key block b2, 32-column block db): 4 transposed reads of 4
+    // keys; element j of the A operand is key 16*ss + 8*(j>>2) + 4*hf + (j&3), the same
+    // key as element j of the P^T B operand.  Inline asm: hipcc cannot prove the builtin
+    // form disjoint from the in-flight LDS-DMA and would drain it (vmcnt(0)) before every
+    // read; vwait() waits for them and names every destination.  Every read is one of two
+    // per-lane base addresses (key rows +0 / +8, whose swizzles differ) plus an immediate:
+    // lds_off(row + 32*b2 + 16*ss, ch + 4*db) = lds_off(row, ch) + (4*b2 + 2*ss)*8*ROWB + 512*db.
+    const unsigned vbase0 = (unsigned)(size_t)smem + lds_off<D>(tr_row, tr_col >> 3) + (tr_col & 7) * 2;
+    const unsigned vbase1 =
+        (unsigned)(size_t)smem + lds_off<D>(tr_row + 8, tr_col >> 3) + (tr_col & 7) * 2 - 8 * ROWB;
+    auto read_v = [](auto slot_c, auto i_c, u32x2 (&vf)[2][2], unsigned vbase0, unsigned vbase1) {
+        constexpr int SLOT = decltype(slot_c)::value, I = decltype(i_c)::value;
+        constexpr int B2 = I / NDB, DB = I % NDB;
+        constexpr int OFF = 2 * TILEB + SLOT * TILEB + 4 * B2 * 8 * ROWB + 512 * DB;
+        constexpr int SSO = 2 * 8 * ROWB;  // +16 key rows (k-step ss = 1)
+        static_assert(OFF + SSO + 8 * ROWB < 65536, "ds offset field is 16 bits");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[0][0]) : "v"(vbase0), "i"(OFF) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[0][1]) : "v"(vbase1), "i"(OFF + 8 * ROWB) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[1][0]) : "v"(vbase0), "i"(OFF + SSO) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[1][1]) : "v"(vbase1), "i"(OFF + SSO + 8 * ROWB) : "memory");
+    };
+    auto vwait = [&](u32x2 (&vf)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(vf[0][0]), "+v"(vf[0][1]), "+v"(vf[1][0]), "+v"(vf[1][1]));
+    };
 
-        // deferred rescale: wave-uniform decision, taken before any P of this tile exists
+    // One pipeline step for tile t, whose raw (masked) scores are in sc and row max in mx:
+    //   DMA K(t+2), V(t+1) into the ring slots freed by the previous step's barrier;
+    //   rescale decision; QK^T(t+1) -> sn interleaved with exp / sum / pack of sc;
+    //   P.V(t) interleaved with mask + row max of sn;  barrier (which also drains the DMA).
+    // P = t & 1 is a compile-time constant (the loop runs steps in pairs).
+    auto step = [&](auto par_c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2], float& mx) {
+        constexpr int P = decltype(par_c)::value;
+        if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(krs, kring + P * TILEB, t + 2);
+        if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
+
         if (__builtin_amdgcn_ballot_w64(mx > m + kThr)) {
             const float m_new = fmaxf(m, mx);
             const float alpha = __builtin_amdgcn_exp2f(m - m_new);
@@ -299,19 +353,31 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
             for (int db = 0; db < NDB; ++db) o[db] *= alpha;
         }
 
-        float sum4[4] = {0.f, 0.f, 0.f, 0.f};
+        const bool more = t + 1 < ntiles;
+        if (more) {
+            // QK^T(t+1) with the exponentials of tile t paced between its MFMAs (MFMA and
+            // VALU pipes busy at once; one basic block so the scheduler can interleave)
+            qk(kring + (1 - P) * TILEB, sn);
+            exp_tile(sc);
+#if FA_QK_SCHED == 1
 #pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[b2][r], c, -m));
-                s[b2][r] = p;
-                sum4[(b2 * 16 + r) & 3] += p;
+            for (int i = 0; i < 2 * NKS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);                   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 96 / (2 * NKS) + 1, 1);  // VALU
             }
-        l += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
-
-        // P^T packed to 16-bit: registers 8*ss .. 8*ss+7 of block b2 form the B operand
-        // of k-step ss; its element j is key 16*ss + 8*(j>>2) + 4*hf + (j&3) of the block.
+#elif FA_QK_SCHED == 2
+            // K reads run FA_QK_LEAD fragments ahead of the MFMAs; VALU fills the gaps
+            __builtin_amdgcn_sched_group_barrier(0x100, FA_QK_LEAD, 1);  // DS_READ
+#pragma unroll
+            for (int i = 0; i < 2 * NKS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+                if (i + FA_QK_LEAD < 2 * NKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x002, 96 / (2 * NKS) + 1, 1);  // VALU
+            }
+#endif
+        } else {
+            exp_tile(sc);
+        }
         v8 pb[2][2];
 #pragma unroll
         for (int b2 = 0; b2 < 2; ++b2)
@@ -319,37 +385,63 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
             for (int ss = 0; ss < 2; ++ss) {
                 u32x4 u;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) u[j] = pack2<T>(s[b2][8 * ss + 2 * j], s[b2][8 * ss + 2 * j + 1]);
+                for (int j = 0; j < 4; ++j) u[j] = pack2<T>(sc[b2][8 * ss + 2 * j], sc[b2][8 * ss + 2 * j + 1]);
                 pb[b2][ss] = __builtin_bit_cast(v8, u);
             }
 
-        // O^T[dv][q] += V^T[dv][key] . P^T[key][q], block db's MFMAs overlapping the
-        // reads of block db+1.
+        // O^T[dv][q] += V^T[dv][key] . P^T[key][q]; reads of the next (b2, db) block
+        // overlap this block's two MFMAs.
+        u32x2 vcur[2][2], vnext[2][2];
+        read_v(par_c, std::integral_constant<int, 0>{}, vcur, vbase0, vbase1);
         vwait(vcur);
+        static_for<2 * NDB>([&](auto i_c) {
+            constexpr int I = decltype(i_c)::value;
+            constexpr int B2 = I / NDB, DB = I % NDB;
+            if constexpr (I + 1 < 2 * NDB)
+                read_v(par_c, std::integral_constant<int, I + 1>{}, vnext, vbase0, vbase1);
 #pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-            u32x2 vnext[2][2][2];
-            if (db + 1 < NDB) read_v(db + 1, vnext);
-#pragma unroll
-            for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    const u32x4 vv = {vcur[b2][ss][0][0], vcur[b2][ss][0][1], vcur[b2][ss][1][0],
-                                      vcur[b2][ss][1][1]};
-                    o[db] = M::mma(__builtin_bit_cast(v8, vv), pb[b2][ss], o[db]);
-                }
-            if (db + 1 < NDB) {
+            for (int ss = 0; ss < 2; ++ss) {
+                const u32x4 vv = {vcur[ss][0][0], vcur[ss][0][1], vcur[ss][1][0], vcur[ss][1][1]};
+#if FA_ABL_NOPV
+                asm volatile("" ::"v"(vv), "v"(pb[B2][ss]));
+#else
+                o[DB] = M::mma(__builtin_bit_cast(v8, vv), pb[B2][ss], o[DB]);
+#endif
+            }
+            if constexpr (I + 1 < 2 * NDB) {
                 vwait(vnext);
 #pragma unroll
-                for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-                    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) vcur[b2][ss][h] = vnext[b2][ss][h];
+                for (int ss = 0; ss < 2; ++ss) {
+                    vcur[ss][0] = vnext[ss][0];
+                    vcur[ss][1] = vnext[ss][1];
+                }
             }
+        });
+        if (more) {
+            mask(t + 1, sn);
+            mx = rowmax(sn);
         }
+        __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
+    };
 
-        __syncthreads();  // hipcc puts vmcnt(0) here: tile t+1's DMA has landed
+    // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
+    dma_tile(krs, kring, 0);
+    dma_tile(vrs, vring, 0);
+    if (ntiles > 1) dma_tile(krs, kring + TILEB, 1);
+    // Q's loads must retire here: otherwise hipcc's waitcnt pass carries them into the loop
+    // header and, merging with the back edge, waits vmcnt(N) in front of every MFMA.
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
+    __syncthreads();
+    f32x16 sa[2], sb[2];
+    qk(kring, sa);
+    mask(0, sa);
+    float mx = rowmax(sa);
+    __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
+
+    for (int t = 0; t < ntiles; t += 2) {
+        step(std::integral_constant<int, 0>{}, t, sa, sb, mx);
+        if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1, sb, sa, mx);
     }
 
     // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (r&3) + 8*(r>>2) + 4*hf

@@ -10,7 +10,10 @@ namespace fa {
 // query rows (one 32x32x16 MFMA column block); a workgroup has kWaves waves.
 constexpr int kBK = 64;
 constexpr int kRowsPerWave = 32;
-constexpr int kWaves = 4;
+#ifndef FA_WAVES
+#define FA_WAVES 4
+#endif
+constexpr int kWaves = FA_WAVES;
 constexpr int kThreads = kWaves * 64;
 constexpr int kBQ = kWaves * kRowsPerWave;
 

@@ -1,0 +1,64 @@
+"""Interleaved A/B timing of several builds of libfa_mi355x.so in ONE process.
+
+    python scripts/ab.py [--config c3] [--rounds 10] lib_a.so lib_b.so ...
+
+Each round times every library once (20 launches, HIP events), rounds interleaved so
+clock / thermal drift hits all variants alike (cdna_hip_programming.md §5.4 rule 24).
+Also checks each variant's output against the first one.
+"""
+import argparse
+import ctypes
+import statistics
+
+import torch
+
+CFG = {"c2": (32, 8, 1024, 32), "c3": (32, 8, 1024, 128), "c3s": (32, 8, 4096, 128),
+       "c4": (32, 8, 4096, 128)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    B, H, L, d = CFG[args.config]
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q, k, v = (torch.randn(B, H, L, d, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    outs = [torch.empty_like(q) for _ in args.libs]
+    libs = []
+    for p in args.libs:
+        h = ctypes.CDLL(p)
+        h.fa_fwd_v1.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64] * 4 + [ctypes.c_int, ctypes.c_void_p]
+        libs.append(h)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run(i):
+        st = libs[i].fa_fwd_v1(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d, 1, stream)
+        assert st == 0, st
+
+    for i in range(len(libs)):
+        for _ in range(5):
+            run(i)
+    torch.cuda.synchronize()
+    times = [[] for _ in libs]
+    for _ in range(args.rounds):
+        for i in range(len(libs)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                run(i)
+            e1.record()
+            torch.cuda.synchronize()
+            times[i].append(e0.elapsed_time(e1) / args.iters)
+    flops = 4.0 * B * H * L * L * d
+    for i, p in enumerate(args.libs):
+        med = statistics.median(times[i])
+        diff = (outs[i].float() - outs[0].float()).abs().max().item()
+        print(f"{p}: median {med * 1e3:.1f} us  min {min(times[i]) * 1e3:.1f} us  "
+              f"{flops / (med * 1e-3) / 1e12:.1f} TFLOP/s  maxdiff_vs_0 {diff:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
