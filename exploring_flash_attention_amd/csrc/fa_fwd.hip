@@ -146,17 +146,19 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, int 
 }
 
 template <typename T, typename PT, int D, bool PARTIAL>
-__global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
+    constexpr int RB = kRB;                   // 32-row query blocks per wave
     constexpr int ROWB = D * 2;               // bytes per LDS row
     constexpr int TILEB = kBK * ROWB;         // bytes of one K (or V) tile
     constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
     constexpr int NDB = D / 32;               // 32-column blocks of O
+    constexpr int NKB = kBK / 32;             // 32-key blocks per KV tile
     // Deferred rescale (defer-max): the reference max m of a row is only moved when some
-    // row of the wave sees a tile max above m + kThr (log2 units); P is then bounded by
-    // 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows (the
-    // dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
+    // row of the wave's block sees a tile max above m + kThr (log2 units); P is then
+    // bounded by 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows
+    // (the dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
     constexpr float kThr = 4.f;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -190,15 +192,16 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     const __amdgpu_buffer_rsrc_t vrs =
         make_rsrc((const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D, (int64_t)nkv * ROWB);
 
-    // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7].  Rows past Lq
-    // read zeros and are never stored.
-    const int64_t q_row = (int64_t)qt * kBQ + wid * kRowsPerWave + l32;
-    v8 qf[NKS];
-    {
-        const int qoff = (int)(q_row * ROWB) + hf * 16;
+    // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7] of each of its
+    // RB row blocks.  Rows past Lq read zeros and are never stored.
+    const int64_t q_row0 = (int64_t)qt * kBQ + wid * kRowsPerWave + l32;
+    v8 qf[RB][NKS];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const int qoff = (int)((q_row0 + 32 * r) * ROWB) + hf * 16;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
-            qf[ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, qoff + ks * 32, 0, 0));
+            qf[r][ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, qoff + ks * 32, 0, 0));
     }
 
     // K/V tiles go HBM -> LDS by LDS-DMA (buffer_load ... lds): no staging VGPRs, no
@@ -230,27 +233,35 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     const int tr_row = 4 * (grp >> 1) + (gi >> 2);
     const int tr_col = 16 * (grp & 1) + 4 * (gi & 3);
 
-    f32x16 o[NDB];
+    f32x16 o[RB][NDB];
 #pragma unroll
-    for (int db = 0; db < NDB; ++db) o[db] = f32x16{};
-    float m = -INFINITY;  // reference max of the row, log2 units (scores * scale_log2)
-    float l = 0.f;        // this lane's half of the running denominator
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) o[r][db] = f32x16{};
+    float m[RB], l[RB];  // reference max (log2 units) and this lane's half of the row sum
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        m[r] = -INFINITY;
+        l[r] = 0.f;
+    }
     const float c = a.scale_log2;
 
-    // S^T[key][q] = K . Q^T for one tile (two 32-key blocks).  K fragments are read in
-    // groups of two k-steps, one group ahead of the MFMAs that consume it.
-    auto qk = [&](const char* kb, f32x16 (&s)[2]) {
+    // S^T[key][q] = K . Q^T for one tile (two 32-key blocks), every K fragment feeding the
+    // RB row blocks.  Fragments are read in groups of two k-steps, one group ahead.
+    auto qk = [&](const char* kb, f32x16 (&s)[RB][NKB]) {
         constexpr int G = 2;  // k-steps per read group
-        v8 kf[2][2][G];       // [buffer][b2][k-step in group]
-        auto rd = [&](int g, v8 (&dst)[2][G]) {
+        v8 kf[2][NKB][G];     // [buffer][b2][k-step in group]
+        auto rd = [&](int g, v8 (&dst)[NKB][G]) {
 #pragma unroll
             for (int j = 0; j < G; ++j)
 #pragma unroll
-                for (int b2 = 0; b2 < 2; ++b2)
+                for (int b2 = 0; b2 < NKB; ++b2)
                     dst[b2][j] = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * (g * G + j) + hf));
         };
-        s[0] = f32x16{};
-        s[1] = f32x16{};
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int b2 = 0; b2 < NKB; ++b2) s[r][b2] = f32x16{};
         rd(0, kf[0]);
 #pragma unroll
         for (int g = 0; g < NKS / G; ++g) {
@@ -258,55 +269,67 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int j = 0; j < G; ++j)
 #pragma unroll
-                for (int b2 = 0; b2 < 2; ++b2) {
+                for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) {
 #if FA_ABL_NOQK
-                    asm volatile("" ::"v"(kf[g & 1][b2][j]));
-                    s[b2][j] += (float)qf[g * G + j][0];
+                        asm volatile("" ::"v"(kf[g & 1][b2][j]));
+                        s[r][b2][j] += (float)qf[r][g * G + j][0];
 #else
-                    s[b2] = M::mma(kf[g & 1][b2][j], qf[g * G + j], s[b2]);
+                        s[r][b2] = M::mma(kf[g & 1][b2][j], qf[r][g * G + j], s[r][b2]);
 #endif
-                }
+                    }
         }
     };
     // P = 2^(S*c - m) in place, and its row sum into l
-    auto exp_tile = [&](f32x16 (&s)[2]) {
-        float sum4[4] = {0.f, 0.f, 0.f, 0.f};
+    auto exp_tile = [&](f32x16 (&s)[RB][NKB]) {
 #pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
+        for (int r = 0; r < RB; ++r) {
+            float sum4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
 #if FA_ABL_NOEXP
-                s[b2][r] = __builtin_fmaf(s[b2][r], c, -m);
+                    s[r][b2][i] = __builtin_fmaf(s[r][b2][i], c, -m[r]);
 #else
-                s[b2][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[b2][r], c, -m));
+                    s[r][b2][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][b2][i], c, -m[r]));
 #endif
-                sum4[(b2 * 16 + r) & 3] += s[b2][r];
-            }
-        l += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
+                    sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
+                }
+            l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
+        }
     };
     // keys past the end of the split (only in the last, partial tile) -> -inf
-    auto mask = [&](int t, f32x16 (&s)[2]) {
+    auto mask = [&](int t, f32x16 (&s)[RB][NKB]) {
         const int valid = nkv - t * kBK;
         if (valid < kBK) {
 #pragma unroll
-            for (int b2 = 0; b2 < 2; ++b2)
+            for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = b2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-                    if (key >= valid) s[b2][r] = -INFINITY;
+                for (int i = 0; i < 16; ++i) {
+                    const int key = b2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+                    if (key >= valid) {
+#pragma unroll
+                        for (int r = 0; r < RB; ++r) s[r][b2][i] = -INFINITY;
+                    }
                 }
         }
     };
     // row max of a (masked) tile, both lane halves, in log2 units
-    auto rowmax = [&](const f32x16 (&s)[2]) {
-        float mx4[4];
+    auto rowmax = [&](const f32x16 (&s)[RB][NKB], float (&mx)[RB]) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mx4[j] = fmaxf(s[j >> 1][8 * (j & 1)], s[j >> 1][8 * (j & 1) + 1]);
+        for (int r = 0; r < RB; ++r) {
+            float mx4[4];  // 4 independent chains over the tile's 16*NKB values
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 4; ++j) mx4[j] = s[r][0][j];
 #pragma unroll
-            for (int r = 2; r < 8; ++r) mx4[j] = fmaxf(mx4[j], s[j >> 1][8 * (j & 1) + r]);
-        return pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
+            for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (b2 > 0 || i >= 4) mx4[i & 3] = fmaxf(mx4[i & 3], s[r][b2][i]);
+            mx[r] = pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
+        }
     };
     // V^T fragments of (32-key block b2, 32-column block db): 4 transposed reads of 4
     // keys; element j of the A operand is key 16*ss + 8*(j>>2) + 4*hf + (j&3), the same
@@ -336,79 +359,72 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
 
     // One pipeline step for tile t, whose raw (masked) scores are in sc and row max in mx:
     //   DMA K(t+2), V(t+1) into the ring slots freed by the previous step's barrier;
-    //   rescale decision; QK^T(t+1) -> sn interleaved with exp / sum / pack of sc;
-    //   P.V(t) interleaved with mask + row max of sn;  barrier (which also drains the DMA).
+    //   rescale decision; QK^T(t+1) -> sn beside exp / sum of sc; pack P;
+    //   P.V(t), then mask + row max of sn;  barrier (which also drains the DMA).
     // P = t & 1 is a compile-time constant (the loop runs steps in pairs).
-    auto step = [&](auto par_c, int t, f32x16 (&sc)[2], f32x16 (&sn)[2], float& mx) {
+    auto step = [&](auto par_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB], float (&mx)[RB]) {
         constexpr int P = decltype(par_c)::value;
         if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(krs, kring + P * TILEB, t + 2);
         if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
 
-        if (__builtin_amdgcn_ballot_w64(mx > m + kThr)) {
-            const float m_new = fmaxf(m, mx);
-            const float alpha = __builtin_amdgcn_exp2f(m - m_new);
-            m = m_new;
-            l *= alpha;
 #pragma unroll
-            for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+        for (int r = 0; r < RB; ++r) {
+            if (__builtin_amdgcn_ballot_w64(mx[r] > m[r] + kThr)) {
+                const float m_new = fmaxf(m[r], mx[r]);
+                const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
+                m[r] = m_new;
+                l[r] *= alpha;
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
+            }
         }
 
         const bool more = t + 1 < ntiles;
         if (more) {
-            // QK^T(t+1) with the exponentials of tile t paced between its MFMAs (MFMA and
-            // VALU pipes busy at once; one basic block so the scheduler can interleave)
+            // QK^T(t+1) and the exponentials of tile t in one basic block: the MFMA and
+            // VALU pipes run side by side
             qk(kring + (1 - P) * TILEB, sn);
             exp_tile(sc);
-#if FA_QK_SCHED == 1
-#pragma unroll
-            for (int i = 0; i < 2 * NKS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);                   // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 96 / (2 * NKS) + 1, 1);  // VALU
-            }
-#elif FA_QK_SCHED == 2
-            // K reads run FA_QK_LEAD fragments ahead of the MFMAs; VALU fills the gaps
-            __builtin_amdgcn_sched_group_barrier(0x100, FA_QK_LEAD, 1);  // DS_READ
-#pragma unroll
-            for (int i = 0; i < 2 * NKS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
-                if (i + FA_QK_LEAD < 2 * NKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-                __builtin_amdgcn_sched_group_barrier(0x002, 96 / (2 * NKS) + 1, 1);  // VALU
-            }
-#endif
         } else {
             exp_tile(sc);
         }
-        v8 pb[2][2];
+        v8 pb[RB][NKB][2];
 #pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
+        for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                u32x4 u;
+            for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) u[j] = pack2<T>(sc[b2][8 * ss + 2 * j], sc[b2][8 * ss + 2 * j + 1]);
-                pb[b2][ss] = __builtin_bit_cast(v8, u);
-            }
+                for (int ss = 0; ss < 2; ++ss) {
+                    u32x4 u;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        u[j] = pack2<T>(sc[r][b2][8 * ss + 2 * j], sc[r][b2][8 * ss + 2 * j + 1]);
+                    pb[r][b2][ss] = __builtin_bit_cast(v8, u);
+                }
 
         // O^T[dv][q] += V^T[dv][key] . P^T[key][q]; reads of the next (b2, db) block
-        // overlap this block's two MFMAs.
+        // overlap this block's MFMAs.
         u32x2 vcur[2][2], vnext[2][2];
         read_v(par_c, std::integral_constant<int, 0>{}, vcur, vbase0, vbase1);
         vwait(vcur);
-        static_for<2 * NDB>([&](auto i_c) {
+        static_for<NKB * NDB>([&](auto i_c) {
             constexpr int I = decltype(i_c)::value;
             constexpr int B2 = I / NDB, DB = I % NDB;
-            if constexpr (I + 1 < 2 * NDB)
+            if constexpr (I + 1 < NKB * NDB)
                 read_v(par_c, std::integral_constant<int, I + 1>{}, vnext, vbase0, vbase1);
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 const u32x4 vv = {vcur[ss][0][0], vcur[ss][0][1], vcur[ss][1][0], vcur[ss][1][1]};
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
 #if FA_ABL_NOPV
-                asm volatile("" ::"v"(vv), "v"(pb[B2][ss]));
+                    asm volatile("" ::"v"(vv), "v"(pb[r][B2][ss]));
 #else
-                o[DB] = M::mma(__builtin_bit_cast(v8, vv), pb[B2][ss], o[DB]);
+                    o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
 #endif
+                }
             }
-            if constexpr (I + 1 < 2 * NDB) {
+            if constexpr (I + 1 < NKB * NDB) {
                 vwait(vnext);
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
@@ -419,7 +435,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
         });
         if (more) {
             mask(t + 1, sn);
-            mx = rowmax(sn);
+            rowmax(sn, mx);
         }
         __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
     };
@@ -431,12 +447,15 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
     // Q's loads must retire here: otherwise hipcc's waitcnt pass carries them into the loop
     // header and, merging with the back edge, waits vmcnt(N) in front of every MFMA.
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[r][ks]));
     __syncthreads();
-    f32x16 sa[2], sb[2];
+    f32x16 sa[RB][NKB], sb[RB][NKB];
+    float mx[RB];
     qk(kring, sa);
     mask(0, sa);
-    float mx = rowmax(sa);
+    rowmax(sa, mx);
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
 
     for (int t = 0; t < ntiles; t += 2) {
@@ -444,43 +463,47 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FwdArgs a) {
         if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1, sb, sa, mx);
     }
 
-    // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (r&3) + 8*(r>>2) + 4*hf
-    const float l_tot = pair_sum(l);
-    const float inv = 1.f / l_tot;
-    if (q_row >= a.Lq) return;
-    if constexpr (!PARTIAL) {
-        unsigned short* Oh = (unsigned short*)a.o + bh * a.Lq * D + q_row * D;
+    // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (i&3) + 8*(i>>2) + 4*hf
 #pragma unroll
-        for (int db = 0; db < NDB; ++db)
+    for (int r = 0; r < RB; ++r) {
+        const int64_t q_row = q_row0 + 32 * r;
+        const float l_tot = pair_sum(l[r]);
+        const float inv = 1.f / l_tot;
+        if (q_row >= a.Lq) continue;
+        if constexpr (!PARTIAL) {
+            unsigned short* Oh = (unsigned short*)a.o + bh * a.Lq * D + q_row * D;
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                u32x2 u;
-                u[0] = pack2<T>(o[db][4 * g4 + 0] * inv, o[db][4 * g4 + 1] * inv);
-                u[1] = pack2<T>(o[db][4 * g4 + 2] * inv, o[db][4 * g4 + 3] * inv);
-                *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
-            }
-    } else {
-        const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
-        const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
-        PT* Op = (PT*)a.o + split * a.split_stride + row_lin * D;
+            for (int db = 0; db < NDB; ++db)
 #pragma unroll
-        for (int db = 0; db < NDB; ++db)
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int col = db * 32 + 8 * g4 + 4 * hf;
-                if constexpr (sizeof(PT) == 4) {
-                    f32x4 f = {o[db][4 * g4 + 0] * inv, o[db][4 * g4 + 1] * inv,
-                               o[db][4 * g4 + 2] * inv, o[db][4 * g4 + 3] * inv};
-                    *(f32x4*)(Op + col) = f;
-                } else {
+                for (int g4 = 0; g4 < 4; ++g4) {
                     u32x2 u;
-                    u[0] = pack2<T>(o[db][4 * g4 + 0] * inv, o[db][4 * g4 + 1] * inv);
-                    u[1] = pack2<T>(o[db][4 * g4 + 2] * inv, o[db][4 * g4 + 3] * inv);
-                    *(u32x2*)((unsigned short*)Op + col) = u;
+                    u[0] = pack2<T>(o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv);
+                    u[1] = pack2<T>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
+                    *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
                 }
-            }
-        // lse in log2 units: m + log2(l)  (v_log_f32 is log2)
-        if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m + __builtin_amdgcn_logf(l_tot);
+        } else {
+            const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
+            const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
+            PT* Op = (PT*)a.o + split * a.split_stride + row_lin * D;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const int col = db * 32 + 8 * g4 + 4 * hf;
+                    if constexpr (sizeof(PT) == 4) {
+                        f32x4 f = {o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv,
+                                   o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv};
+                        *(f32x4*)(Op + col) = f;
+                    } else {
+                        u32x2 u;
+                        u[0] = pack2<T>(o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv);
+                        u[1] = pack2<T>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
+                        *(u32x2*)((unsigned short*)Op + col) = u;
+                    }
+                }
+            // lse in log2 units: m + log2(l)  (v_log_f32 is log2)
+            if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m[r] + __builtin_amdgcn_logf(l_tot);
+        }
     }
 }
 

@@ -6,16 +6,29 @@
 
 namespace fa {
 
-// Keys per KV tile and query rows per wave of the forward kernel.  A wave owns 32
-// query rows (one 32x32x16 MFMA column block); a workgroup has kWaves waves.
-constexpr int kBK = 64;
-constexpr int kRowsPerWave = 32;
+// Keys per KV tile and query rows per wave of the forward kernel.  A wave owns kRB
+// blocks of 32 query rows (one 32x32x16 MFMA column block each) and every K / V
+// fragment it reads from LDS feeds kRB MFMAs; a workgroup has kWaves waves.
+//   kRB = 1: 32 rows per wave, <= 256 registers, two waves per SIMD (default);
+//   kRB = 2: 64 rows per wave, ~460 registers, ONE wave per SIMD -- halves the LDS
+//            fragment traffic per MFMA, but hipcc's schedule for it (AGPR shuffling, no
+//            second wave to hide latency) measured 1.6x slower at C3 (profiles/).
 #ifndef FA_WAVES
 #define FA_WAVES 4
 #endif
+#ifndef FA_RB
+#define FA_RB 1
+#endif
+#ifndef FA_BK
+#define FA_BK (FA_RB == 1 ? 64 : 32)
+#endif
+constexpr int kBK = FA_BK;  // keys per KV tile (a multiple of 32)
+constexpr int kRB = FA_RB;
+constexpr int kRowsPerWave = 32 * kRB;
 constexpr int kWaves = FA_WAVES;
 constexpr int kThreads = kWaves * 64;
 constexpr int kBQ = kWaves * kRowsPerWave;
+constexpr int kWavesPerSimd = kRB == 1 ? 2 : 1;  // occupancy the register budget is sized for
 
 enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2 };
 
