@@ -362,8 +362,14 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     //   rescale decision; QK^T(t+1) -> sn beside exp / sum of sc; pack P;
     //   P.V(t), then mask + row max of sn;  barrier (which also drains the DMA).
     // P = t & 1 is a compile-time constant (the loop runs steps in pairs).
-    auto step = [&](auto par_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB], float (&mx)[RB]) {
+    auto step = [&](auto par_c, auto more_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
+                    float (&mx)[RB]) {
         constexpr int P = decltype(par_c)::value;
+        // MORE: a tile t+1 exists.  Compile-time, so QK^T(t+1), the exponentials, the
+        // packing and P.V(t) form ONE basic block the scheduler can interleave (a runtime
+        // `if` let hipcc hoist the shared exp code into the join block, away from the
+        // MFMAs).
+        constexpr bool MORE = decltype(more_c)::value;
         if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(krs, kring + P * TILEB, t + 2);
         if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
 
@@ -379,15 +385,8 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
             }
         }
 
-        const bool more = t + 1 < ntiles;
-        if (more) {
-            // QK^T(t+1) and the exponentials of tile t in one basic block: the MFMA and
-            // VALU pipes run side by side
-            qk(kring + (1 - P) * TILEB, sn);
-            exp_tile(sc);
-        } else {
-            exp_tile(sc);
-        }
+        if constexpr (MORE) qk(kring + (1 - P) * TILEB, sn);
+        exp_tile(sc);
         v8 pb[RB][NKB][2];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
@@ -433,7 +432,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
                 }
             }
         });
-        if (more) {
+        if constexpr (MORE) {
             mask(t + 1, sn);
             rowmax(sn, mx);
         }
@@ -458,9 +457,22 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     rowmax(sa, mx);
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
 
-    for (int t = 0; t < ntiles; t += 2) {
-        step(std::integral_constant<int, 0>{}, t, sa, sb, mx);
-        if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1, sb, sa, mx);
+    {
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using YES = std::integral_constant<bool, true>;
+        using NO = std::integral_constant<bool, false>;
+        int t = 0;
+        for (; t + 2 < ntiles; t += 2) {
+            step(C0{}, YES{}, t, sa, sb, mx);
+            step(C1{}, YES{}, t + 1, sb, sa, mx);
+        }
+        if (ntiles - t == 2) {  // t is even here
+            step(C0{}, YES{}, t, sa, sb, mx);
+            step(C1{}, NO{}, t + 1, sb, sa, mx);
+        } else {
+            step(C0{}, NO{}, t, sa, sb, mx);
+        }
     }
 
     // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (i&3) + 8*(i>>2) + 4*hf
