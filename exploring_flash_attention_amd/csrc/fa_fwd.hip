@@ -37,6 +37,9 @@
 #ifndef FA_QK_SCHED
 #define FA_QK_SCHED 0
 #endif
+#ifndef FA_WIDE_STORE
+#define FA_WIDE_STORE 1
+#endif
 #ifndef FA_ABL_NOEXP
 #define FA_ABL_NOEXP 0
 #endif
@@ -484,6 +487,25 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
         if (q_row >= a.Lq) continue;
         if constexpr (!PARTIAL) {
             unsigned short* Oh = (unsigned short*)a.o + bh * a.Lq * D + q_row * D;
+#if FA_WIDE_STORE
+            // Column groups g and g+1 of a row sit in lanes l (cols 8g..+3, 8g+8..+11) and
+            // l+32 (8g+4..+7, 8g+12..+15); one v_permlane32_swap per dword leaves 16
+            // contiguous bytes in each lane -> one dwordx4 store per pair instead of two
+            // dwordx2 (cdna_hip_programming.md T21).
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int gp = 0; gp < 4; gp += 2) {
+                    unsigned x0 = pack2<T>(o[r][db][4 * gp + 0] * inv, o[r][db][4 * gp + 1] * inv);
+                    unsigned x1 = pack2<T>(o[r][db][4 * gp + 2] * inv, o[r][db][4 * gp + 3] * inv);
+                    unsigned y0 = pack2<T>(o[r][db][4 * gp + 4] * inv, o[r][db][4 * gp + 5] * inv);
+                    unsigned y1 = pack2<T>(o[r][db][4 * gp + 6] * inv, o[r][db][4 * gp + 7] * inv);
+                    const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+                    const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
+                    *(u32x4*)(Oh + db * 32 + 8 * gp + 8 * hf) = u;
+                }
+#else
 #pragma unroll
             for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -493,6 +515,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
                     u[1] = pack2<T>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
                     *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
                 }
+#endif
         } else {
             const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
             const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
