@@ -122,8 +122,11 @@ def load_traffic(config):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=20)
+    # The MI355X clock ramps up over the first ~50 ms of back-to-back launches (measured:
+    # 183 / 161 / 149 us per C3 step after 20 / 100 / 400 steps), so the defaults time the
+    # steady state: 300 untimed steps, then 500 timed (~0.1 s in all).
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--mode", default="heads", choices=["heads", "splitkv-dist"])
     ap.add_argument("--cpu-heads", type=int, default=0, help="CPU baseline sample (0 = min(16, cores))")

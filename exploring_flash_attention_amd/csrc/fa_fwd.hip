@@ -40,6 +40,15 @@
 #ifndef FA_WIDE_STORE
 #define FA_WIDE_STORE 1
 #endif
+// FA_MFMA_ROWSUM: the softmax denominator as one more MFMA column block (ones . P^T)
+// instead of 32 VALU adds per tile: sums the same 16-bit-rounded P the numerator uses.
+// Default: on for d <= 32 (VALU-bound, +4 %), off for larger d (MFMA-heavier, -4 %).
+#ifndef FA_MFMA_ROWSUM_MAXD
+#define FA_MFMA_ROWSUM_MAXD 32
+#endif
+#ifndef FA_ABL_NODMAWAIT
+#define FA_ABL_NODMAWAIT 0
+#endif
 #ifndef FA_ABL_NOEXP
 #define FA_ABL_NOEXP 0
 #endif
@@ -163,6 +172,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     // bounded by 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows
     // (the dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
     constexpr float kThr = 4.f;
+    constexpr bool FA_MFMA_ROWSUM = D <= FA_MFMA_ROWSUM_MAXD;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: K ring (2 slots) then V ring (2 slots), one [kBK][D] tile image per slot.
@@ -242,6 +252,12 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
 #pragma unroll
         for (int db = 0; db < NDB; ++db) o[r][db] = f32x16{};
     float m[RB], l[RB];  // reference max (log2 units) and this lane's half of the row sum
+    f32x16 lsum[RB];     // FA_MFMA_ROWSUM: every register = the row sum of the lane's query
+#pragma unroll
+    for (int r = 0; r < RB; ++r) lsum[r] = f32x16{};
+    v8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = static_cast<T>(1.0f);
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         m[r] = -INFINITY;
@@ -298,9 +314,9 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
 #else
                     s[r][b2][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][b2][i], c, -m[r]));
 #endif
-                    sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
+                    if (!FA_MFMA_ROWSUM) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
                 }
-            l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
+            if (!FA_MFMA_ROWSUM) l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
         }
     };
     // keys past the end of the split (only in the last, partial tile) -> -inf
@@ -383,6 +399,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
                 const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
                 m[r] = m_new;
                 l[r] *= alpha;
+                if (FA_MFMA_ROWSUM) lsum[r] *= alpha;
 #pragma unroll
                 for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
             }
@@ -424,6 +441,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
 #else
                     o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
 #endif
+                    if (FA_MFMA_ROWSUM && DB == 0) lsum[r] = M::mma(ones, pb[r][B2][ss], lsum[r]);
                 }
             }
             if constexpr (I + 1 < NKB * NDB) {
@@ -439,7 +457,12 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
             mask(t + 1, sn);
             rowmax(sn, mx);
         }
+#if FA_ABL_NODMAWAIT
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#else
         __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
+#endif
     };
 
     // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
@@ -482,7 +505,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         const int64_t q_row = q_row0 + 32 * r;
-        const float l_tot = pair_sum(l[r]);
+        const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
         const float inv = 1.f / l_tot;
         if (q_row >= a.Lq) continue;
         if constexpr (!PARTIAL) {
