@@ -46,6 +46,12 @@
 #ifndef FA_MFMA_ROWSUM_MAXD
 #define FA_MFMA_ROWSUM_MAXD 32
 #endif
+#ifndef FA_DMA_LATE
+#define FA_DMA_LATE 1
+#endif
+#ifndef FA_PRIO
+#define FA_PRIO 0
+#endif
 #ifndef FA_ABL_NODMAWAIT
 #define FA_ABL_NODMAWAIT 0
 #endif
@@ -389,8 +395,10 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
         // `if` let hipcc hoist the shared exp code into the join block, away from the
         // MFMAs).
         constexpr bool MORE = decltype(more_c)::value;
+#if !FA_DMA_LATE
         if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(krs, kring + P * TILEB, t + 2);
         if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
+#endif
 
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
@@ -405,6 +413,15 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
             }
         }
 
+#if FA_DMA_LATE
+        // DMA issued in the MFMA block (the scheduler spreads the pieces among the MFMAs);
+        // tile counts are checked against the compile-time MORE where possible
+        if (!FA_ABL_NODMA && (MORE && t + 2 < ntiles)) dma_tile(krs, kring + P * TILEB, t + 2);
+        if (!FA_ABL_NODMA && MORE) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
+#endif
+#if FA_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
         if constexpr (MORE) qk(kring + (1 - P) * TILEB, sn);
         exp_tile(sc);
         v8 pb[RB][NKB][2];
@@ -461,6 +478,9 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
 #else
+#if FA_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
 #endif
     };
