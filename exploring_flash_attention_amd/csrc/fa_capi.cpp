@@ -97,8 +97,8 @@ fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int6
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-int splits_for(int64_t L, int kvtpb, int* kv_per_split) {
-    const int64_t keys = (int64_t)kvtpb * fa::kBK;
+int splits_for(int64_t L, int64_t d, int kvtpb, int* kv_per_split) {
+    const int64_t keys = (int64_t)kvtpb * fa::bk_for((int)d);
     *kv_per_split = (int)(keys < L ? keys : L);
     return (int)((L + keys - 1) / keys);
 }
@@ -117,7 +117,7 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
     if (!supported_d(d))
         return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel", (long long)d);
     if (bq) *bq = fa::kBQ;
-    if (bk) *bk = fa::kBK;
+    if (bk) *bk = fa::bk_for((int)d);
     if (threads) *threads = fa::kThreads;
     if (lds_bytes) *lds_bytes = fa::fwd_lds_bytes((int)d);
     return ok();
@@ -158,7 +158,7 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_
         return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
     int kvps;
-    const int ns = splits_for(L, kv_tiles_per_block, &kvps);
+    const int ns = splits_for(L, d, kv_tiles_per_block, &kvps);
     const size_t esz = pe == fa::Elem::F32 ? 4 : 2;
     const size_t rows = (size_t)ns * B * H * L;
     *bytes = align256(rows * d * esz) + align256(rows * sizeof(float));
@@ -192,7 +192,7 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
 
     fa::FwdArgs a = base_args(q, k, v, o_part, BH, L, L, d);
     int kvps;
-    a.nsplit = splits_for(L, kv_tiles_per_block, &kvps);
+    a.nsplit = splits_for(L, d, kv_tiles_per_block, &kvps);
     a.kv_per_split = kvps;
     a.lse = lse;
     a.chunk_rows = L;

@@ -42,15 +42,18 @@
 #endif
 // FA_MFMA_ROWSUM: the softmax denominator as one more MFMA column block (ones . P^T)
 // instead of 32 VALU adds per tile: sums the same 16-bit-rounded P the numerator uses.
-// Default: on for d <= 32 (VALU-bound, +4 %), off for larger d (MFMA-heavier, -4 %).
+// Default off: -4 % at d=128, within noise at d=32 (A/B).
 #ifndef FA_MFMA_ROWSUM_MAXD
-#define FA_MFMA_ROWSUM_MAXD 32
+#define FA_MFMA_ROWSUM_MAXD 0
 #endif
 #ifndef FA_DMA_LATE
 #define FA_DMA_LATE 1
 #endif
 #ifndef FA_PRIO
 #define FA_PRIO 0
+#endif
+#ifndef FA_ROWMAX_FENCE
+#define FA_ROWMAX_FENCE 1
 #endif
 #ifndef FA_ABL_NODMAWAIT
 #define FA_ABL_NODMAWAIT 0
@@ -169,6 +172,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     using v8 = typename M::v8;
     constexpr int RB = kRB;                   // 32-row query blocks per wave
     constexpr int ROWB = D * 2;               // bytes per LDS row
+    constexpr int kBK = bk_for(D);            // keys per KV tile
     constexpr int TILEB = kBK * ROWB;         // bytes of one K (or V) tile
     constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
     constexpr int NDB = D / 32;               // 32-column blocks of O
@@ -206,10 +210,12 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     // (partial) tile reads zeros past kv_end with no clamping code.
     const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D;
     const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, a.Lq * ROWB);
-    const __amdgpu_buffer_rsrc_t krs =
-        make_rsrc((const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D, (int64_t)nkv * ROWB);
-    const __amdgpu_buffer_rsrc_t vrs =
-        make_rsrc((const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D, (int64_t)nkv * ROWB);
+    // K/V of this split; a tile's descriptor (made per DMA, scalar arithmetic only) starts
+    // at the tile and ends at the split's last key, so the hardware range check -- which
+    // does not rely on soffset -- zero-fills the rows of a partial last tile.
+    const unsigned short* const kbase = (const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D;
+    const unsigned short* const vbase = (const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D;
+    const int64_t kv_bytes = (int64_t)nkv * ROWB;
 
     // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7] of each of its
     // RB row blocks.  Rows past Lq read zeros and are never stored.
@@ -240,10 +246,13 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
         const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
         dma_src[i] = row * ROWB + ch * 16;
     }
-    auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, char* slot, int t) {
+    auto dma_tile = [&](const unsigned short* base, char* slot, int t) {
+        const int64_t off = (int64_t)t * TILEB;
+        const __amdgpu_buffer_rsrc_t rs =
+            make_rsrc((const char*)base + off, kv_bytes > off ? kv_bytes - off : 0);
         if (NDMA >= kWaves || dma_wave) {
 #pragma unroll
-            for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], t * TILEB);
+            for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], 0);
         }
     };
 
@@ -387,17 +396,21 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     //   rescale decision; QK^T(t+1) -> sn beside exp / sum of sc; pack P;
     //   P.V(t), then mask + row max of sn;  barrier (which also drains the DMA).
     // P = t & 1 is a compile-time constant (the loop runs steps in pairs).
-    auto step = [&](auto par_c, auto more_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
+    auto step = [&](auto par_c, auto flags_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
                     float (&mx)[RB]) {
         constexpr int P = decltype(par_c)::value;
-        // MORE: a tile t+1 exists.  Compile-time, so QK^T(t+1), the exponentials, the
-        // packing and P.V(t) form ONE basic block the scheduler can interleave (a runtime
-        // `if` let hipcc hoist the shared exp code into the join block, away from the
-        // MFMAs).
-        constexpr bool MORE = decltype(more_c)::value;
+        // Compile-time step flags, so that QK^T(t+1), the exponentials, the packing, P.V(t)
+        // and the row max of tile t+1 form ONE basic block the scheduler can interleave
+        // (runtime `if`s split it: hipcc hoisted the shared exp code into a join block,
+        // away from the MFMAs).
+        //   MORE      tile t+1 exists
+        //   MASKNEXT  tile t+1 may be the partial last tile (needs the key mask)
+        //   DMAK      tile t+2 exists (its K is prefetched now)
+        constexpr int F = decltype(flags_c)::value;
+        constexpr bool MORE = F & 1, MASKNEXT = F & 2, DMAK = F & 4;
 #if !FA_DMA_LATE
-        if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(krs, kring + P * TILEB, t + 2);
-        if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
+        if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(kbase, kring + P * TILEB, t + 2);
+        if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
 #endif
 
 #pragma unroll
@@ -416,8 +429,8 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
 #if FA_DMA_LATE
         // DMA issued in the MFMA block (the scheduler spreads the pieces among the MFMAs);
         // tile counts are checked against the compile-time MORE where possible
-        if (!FA_ABL_NODMA && (MORE && t + 2 < ntiles)) dma_tile(krs, kring + P * TILEB, t + 2);
-        if (!FA_ABL_NODMA && MORE) dma_tile(vrs, vring + (1 - P) * TILEB, t + 1);
+        if constexpr (!FA_ABL_NODMA && DMAK) dma_tile(kbase, kring + P * TILEB, t + 2);
+        if constexpr (!FA_ABL_NODMA && MORE) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
 #endif
 #if FA_PRIO
         __builtin_amdgcn_s_setprio(1);
@@ -471,7 +484,10 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
             }
         });
         if constexpr (MORE) {
-            mask(t + 1, sn);
+#if FA_ROWMAX_FENCE
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            if constexpr (MASKNEXT) mask(t + 1, sn);
             rowmax(sn, mx);
         }
 #if FA_ABL_NODMAWAIT
@@ -486,9 +502,9 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     };
 
     // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
-    dma_tile(krs, kring, 0);
-    dma_tile(vrs, vring, 0);
-    if (ntiles > 1) dma_tile(krs, kring + TILEB, 1);
+    dma_tile(kbase, kring, 0);
+    dma_tile(vbase, vring, 0);
+    if (ntiles > 1) dma_tile(kbase, kring + TILEB, 1);
     // Q's loads must retire here: otherwise hipcc's waitcnt pass carries them into the loop
     // header and, merging with the back edge, waits vmcnt(N) in front of every MFMA.
 #pragma unroll
@@ -506,18 +522,24 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     {
         using C0 = std::integral_constant<int, 0>;
         using C1 = std::integral_constant<int, 1>;
-        using YES = std::integral_constant<bool, true>;
-        using NO = std::integral_constant<bool, false>;
+        // flags: 1 = MORE, 2 = MASKNEXT, 4 = DMAK (see step)
+        using STEADY = std::integral_constant<int, 1 | 4>;     // t+1, t+2 exist, t+1 not last
+        using NEXTLAST = std::integral_constant<int, 1 | 2>;   // t+1 is the last tile
+        using NEXTLASTK = std::integral_constant<int, 1 | 2 | 4>;
+        using LAST = std::integral_constant<int, 0>;
         int t = 0;
         for (; t + 2 < ntiles; t += 2) {
-            step(C0{}, YES{}, t, sa, sb, mx);
-            step(C1{}, YES{}, t + 1, sb, sa, mx);
+            // step t: tile t+1 is never the last one here.  Step t+1 may prefetch K(t+3)
+            // past the end: the buffer range check turns it into zeros nobody reads, which
+            // keeps the step branch-free.
+            step(C0{}, STEADY{}, t, sa, sb, mx);
+            step(C1{}, NEXTLASTK{}, t + 1, sb, sa, mx);
         }
         if (ntiles - t == 2) {  // t is even here
-            step(C0{}, YES{}, t, sa, sb, mx);
-            step(C1{}, NO{}, t + 1, sb, sa, mx);
+            step(C0{}, NEXTLAST{}, t, sa, sb, mx);
+            step(C1{}, LAST{}, t + 1, sb, sa, mx);
         } else {
-            step(C0{}, NO{}, t, sa, sb, mx);
+            step(C0{}, LAST{}, t, sa, sb, mx);
         }
     }
 
@@ -585,7 +607,7 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     }
 }
 
-int fwd_lds_bytes(int d) { return 2 * 2 * kBK * d * 2; }
+int fwd_lds_bytes(int d) { return 2 * 2 * bk_for(d) * d * 2; }
 
 template <typename T, typename PT, int D, bool PARTIAL>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {

@@ -19,10 +19,18 @@ namespace fa {
 #ifndef FA_RB
 #define FA_RB 1
 #endif
-#ifndef FA_BK
-#define FA_BK (FA_RB == 1 ? 64 : 32)
+// Keys per KV tile, per head dim (a multiple of 32).  Small d has registers to spare and
+// is bound by per-tile overheads, so it takes longer tiles.
+#ifndef FA_BK32
+#define FA_BK32 (FA_RB == 1 ? 64 : 32)
 #endif
-constexpr int kBK = FA_BK;  // keys per KV tile (a multiple of 32)
+#ifndef FA_BK64
+#define FA_BK64 (FA_RB == 1 ? 64 : 32)
+#endif
+#ifndef FA_BK128
+#define FA_BK128 (FA_RB == 1 ? 64 : 32)
+#endif
+constexpr int bk_for(int d) { return d <= 32 ? FA_BK32 : d <= 64 ? FA_BK64 : FA_BK128; }
 constexpr int kRB = FA_RB;
 constexpr int kRowsPerWave = 32 * kRB;
 constexpr int kWaves = FA_WAVES;
@@ -44,7 +52,7 @@ struct FwdArgs {
     int64_t Lk;
     int nqt;                 // query tiles per head = ceil(Lq / kBQ)
     int nsplit;              // key splits per head
-    int kv_per_split;        // keys per split, multiple of kBK (Lk for a single split)
+    int kv_per_split;        // keys per split, multiple of bk_for(d) (Lk for a single split)
     int64_t chunk_rows;      // partial: output row chunking (divides Lq)
     int64_t split_stride;    // partial: elements between splits of o_part
     float scale_log2;        // log2(e) / sqrt(d)

@@ -28,7 +28,7 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-        python bench.py --no-cpu-baseline --no-extra --steps 50 --warmup 10 > $OUT/prof.log 2>&1; rc=$?
+        python bench.py --no-cpu-baseline --no-extra > $OUT/prof.log 2>&1; rc=$?
       echo "prof rc=$rc"; tail -3 $OUT/prof.log; stop_if_crash $rc prof
       find $OUT/prof -name "*kernel_stats.csv" -exec cat {} \; | head -20 ;;
   esac
