@@ -13,7 +13,11 @@ ROCm device is present.
 from . import ops  # noqa: F401
 from .ops import (attention_partial, attention_tiled_d, attention_v1, attention_v2,  # noqa: F401
                   combine, kernel_geometry)
+from .tiled_d import flash_attention_v1_tiled_d  # noqa: F401
+from .v1 import flash_attention_v1  # noqa: F401
+from .v2 import flash_attention_v2  # noqa: F401
 
 __all__ = ["ops", "attention_v1", "attention_tiled_d", "attention_v2", "attention_partial",
-           "combine", "kernel_geometry"]
+           "combine", "kernel_geometry", "flash_attention_v1", "flash_attention_v1_tiled_d",
+           "flash_attention_v2"]
 __version__ = "0.1.0"

@@ -30,19 +30,41 @@ def compute_dtype(*arrays):
 
 
 def to_device(arrays, dtype):
-    """Host [L, d] arrays -> contiguous [1, 1, L, d] device tensors of dtype."""
+    """Host [L, d] (or [B, H, L, d]) arrays -> contiguous [B, H, L, d] device tensors."""
     require_gpu()
     dev = torch.device("cuda", torch.cuda.current_device())
     out = []
     for a in arrays:
         t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
-        out.append(t.to(device=dev, dtype=dtype, non_blocking=False)[None, None].contiguous())
+        t = t.to(device=dev, dtype=dtype, non_blocking=False)
+        out.append((t[None, None] if t.dim() == 2 else t).contiguous())
     return out
 
 
-def to_host(t, like_dtype):
-    """[1, 1, L, d] device tensor -> host [L, d] array of like_dtype."""
-    return t[0, 0].float().cpu().numpy().astype(like_dtype, copy=False)
+def to_host(t, like_dtype, ndim=2):
+    """[B, H, L, d] device tensor -> host array of like_dtype ([L, d] when ndim == 2)."""
+    t = t[0, 0] if ndim == 2 else t
+    return t.float().cpu().numpy().astype(like_dtype, copy=False)
+
+
+def run_qkv(fn, Q, K, V):
+    """Apply ``fn(q, k, v) -> o`` (device [B, H, L, d] tensors) to any of the accepted forms:
+
+    * torch device tensors, [B, H, L, d] or [L, d] (zero-copy; result on the device);
+    * host NumPy arrays (or anything ``np.asarray`` takes), [L, d] or [B, H, L, d]
+      (copied in and out; result in Q's dtype, float64 for non-float input).
+    """
+    if is_device_tensor(Q):
+        if Q.dim() == 2:
+            return fn(Q[None, None].contiguous(), K[None, None].contiguous(),
+                      V[None, None].contiguous())[0, 0]
+        return fn(Q, K, V)
+    Q, K, V = (np.asarray(x) for x in (Q, K, V))
+    assert Q.ndim in (2, 4), f"Q must be [L, d] or [B, H, L, d], got shape {Q.shape}"
+    assert K.ndim == Q.ndim and V.ndim == Q.ndim, "Q, K, V must have the same rank"
+    like = Q.dtype if np.issubdtype(Q.dtype, np.floating) else np.float64
+    q, k, v = to_device((Q, K, V), compute_dtype(Q, K, V))
+    return to_host(fn(q, k, v), like, Q.ndim)
 
 
 def is_device_tensor(x):

@@ -52,8 +52,16 @@ def flash_attention_tiled(Q, K, V, O, L, d, Bq=8, Bk=8, d_tile_qk=16, d_tile_v=1
     O[:L * d] = flash_attention_tiled_global(q2, k2, v2, Bq, Bk, d_tile_qk, d_tile_v).reshape(-1)
 
 
-def flash_attention_v1_tiled_d(Q, K, V, O, B, H, L, d, d_tile_qk=32, d_tile_v=32):
-    """Device launcher surface (asynchronous on the current stream)."""
+def flash_attention_v1_tiled_d(Q, K, V, O=None, B=None, H=None, L=None, d=None, d_tile_qk=32,
+                               d_tile_v=32):
+    """``flash_attention_v1_tiled_d(Q, K, V, d_tile_qk=32, d_tile_v=32) -> O`` (host or
+    device), or the launcher form ``(Q, K, V, O, B, H, L, d, d_tile_qk, d_tile_v)``
+    (asynchronous on the current stream)."""
+    if O is None:
+        dd = int(Q.shape[-1])
+        assert 0 < d_tile_qk <= dd and 0 < d_tile_v <= dd, "d_tile must be valid"
+        return _host.run_qkv(lambda q, k, v: ops.attention_tiled_d(q, k, v, d_tile_qk, d_tile_v),
+                             Q, K, V)
     assert B > 0 and H > 0 and L > 0 and d > 0, "All dimensions must be positive"
     assert tuple(Q.shape) == (B, H, L, d), f"Q shape {tuple(Q.shape)} != {(B, H, L, d)}"
     assert 0 < d_tile_qk <= d and 0 < d_tile_v <= d, "d_tile must be valid"

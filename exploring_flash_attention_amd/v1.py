@@ -10,6 +10,8 @@ Reference surfaces mirrored (tyler-utah/exploring_flash_attention):
 * ``flash_attention_v1(Q, K, V, O, B, H, L, d)`` and ``flash_attention_v1_opt1(...)``
       flash_attention_v1/CUDA/flash_attention_v1.h:251, flash_attention_v1_opt1.h:354
       (device [B, H, L, d] tensors, O written in place)
+* ``flash_attention_v1(Q, K, V) -> O`` -- the ``naive_attention(Q, K, V)`` form
+      (common/reference.py:7): NumPy [L, d] / [B, H, L, d] or torch device tensors
 
 ``Bq`` / ``Bk`` are the reference's tile sizes; they are accepted and validated (> 0) but
 the gfx950 kernel uses its own tiles (128 query rows x 64 keys, see
@@ -56,8 +58,12 @@ def flash_attention_tiled(Q, K, V, *args, Bq=8, Bk=8, **kw):
     return _run_host(Q, K, V)
 
 
-def flash_attention_v1(Q, K, V, O, B, H, L, d):
-    """Device launcher surface: O[B,H,L,d] = attention(Q,K,V) (asynchronous on the stream)."""
+def flash_attention_v1(Q, K, V, O=None, B=None, H=None, L=None, d=None):
+    """``flash_attention_v1(Q, K, V) -> O`` (host or device), or the launcher form
+    ``flash_attention_v1(Q, K, V, O, B, H, L, d)``: O[B,H,L,d] written in place,
+    asynchronous on the current stream."""
+    if O is None:
+        return _host.run_qkv(ops.attention_v1, Q, K, V)
     assert B > 0 and H > 0 and L > 0 and d > 0, "All dimensions must be positive"
     assert tuple(Q.shape) == (B, H, L, d), f"Q shape {tuple(Q.shape)} != {(B, H, L, d)}"
     ops.attention_v1(Q, K, V, out=O)

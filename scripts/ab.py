@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=300)
     args = ap.parse_args()
     B, H, L, d = CFG[args.config]
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -41,6 +42,8 @@ def main():
     for i in range(len(libs)):
         for _ in range(5):
             run(i)
+    for _ in range(args.warmup):  # clock ramp: ~50 ms of back-to-back work first
+        run(0)
     torch.cuda.synchronize()
     times = [[] for _ in libs]
     for _ in range(args.rounds):

@@ -55,6 +55,33 @@ def _gate(out, ref, dtype):
 # golden fixtures through the reference-mirroring surfaces
 # ----------------------------------------------------------------------------------------
 
+
+def test_qkv_surfaces(gpu):
+    """``flash_attention_v1/_tiled_d/_v2(Q, K, V) -> O`` (the naive_attention(Q, K, V) form,
+    common/reference.py:7) on NumPy [L, d], NumPy [B, H, L, d] and torch device tensors."""
+    import exploring_flash_attention_amd as fa
+    g = golden("g1_v1_basic_f64.npz")
+    fns = (fa.flash_attention_v1,
+           lambda Q, K, V: fa.flash_attention_v1_tiled_d(Q, K, V, d_tile_qk=16, d_tile_v=16),
+           lambda Q, K, V: fa.flash_attention_v2(Q, K, V, kv_tiles_per_block=1))
+    for fn in fns:
+        O = fn(g["Q"], g["K"], g["V"])  # host [L, d] fp64 -> fp16 kernel -> fp64
+        assert isinstance(O, np.ndarray) and O.dtype == np.float64 and O.shape == g["Q"].shape
+        check_accuracy(O, g["O"])
+        assert np.abs(O - g["O"]).max() <= 3e-3
+    q, k, v = _inputs(2, 3, 130, 64, torch.bfloat16, seed=7)
+    ref = _ref(q, k, v)
+    for fn in fns:
+        O4 = fn(q.float().numpy(), k.float().numpy(), v.float().numpy())  # host [B, H, L, d]
+        assert O4.shape == tuple(q.shape) and O4.dtype == np.float32
+        check_accuracy(O4, ref)
+        od = fn(q.cuda(), k.cuda(), v.cuda())  # device, zero-copy
+        assert od.is_cuda and od.dtype == torch.bfloat16 and tuple(od.shape) == tuple(q.shape)
+        _gate(od, ref, torch.bfloat16)
+        o2 = fn(q[1, 2].cuda(), k[1, 2].cuda(), v[1, 2].cuda())  # device [L, d]
+        assert tuple(o2.shape) == (130, 64)
+        _gate(o2[None, None], ref[1:2, 2:3], torch.bfloat16)
+
 def test_golden_v1_numpy_surface(gpu):
     from exploring_flash_attention_amd import v1
     for name, atol in (("g1_v1_basic_f64.npz", 3e-3), ("g1_v1_basic_f16.npz", 3e-3),
