@@ -33,7 +33,7 @@ int ok() {
     return FA_OK;
 }
 
-bool supported_d(int64_t d) { return d == 32 || d == 64 || d == 128; }
+bool supported_d(int64_t d) { return d == 32 || d == 64 || d == 128 || d == 256; }
 
 int check_dtype(int dtype, fa::Elem* e) {
     if (dtype == FA_DTYPE_BF16) { *e = fa::Elem::BF16; return FA_OK; }
@@ -53,7 +53,7 @@ int check_shape(int64_t B, int64_t H, int64_t L, int64_t d) {
         return fail(FA_ERR_INVALID_ARG, "all dimensions must be positive (B=%lld H=%lld L=%lld d=%lld)",
                     (long long)B, (long long)H, (long long)L, (long long)d);
     if (!supported_d(d))
-        return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel (supported: 32, 64, 128)",
+        return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel (supported: 32, 64, 128, 256)",
                     (long long)d);
     if (L > (int64_t)1 << 30)
         return fail(FA_ERR_UNSUPPORTED, "L=%lld exceeds 2^30", (long long)L);

@@ -76,6 +76,7 @@ static hipError_t launch_c(int d, const CombineArgs& a, hipStream_t s) {
         case 32: hipLaunchKernelGGL((fa_combine_kernel<T, PT, 32>), grid, dim3(256), 0, s, a); break;
         case 64: hipLaunchKernelGGL((fa_combine_kernel<T, PT, 64>), grid, dim3(256), 0, s, a); break;
         case 128: hipLaunchKernelGGL((fa_combine_kernel<T, PT, 128>), grid, dim3(256), 0, s, a); break;
+        case 256: hipLaunchKernelGGL((fa_combine_kernel<T, PT, 256>), grid, dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -167,7 +167,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, int 
 }
 
 template <typename T, typename PT, int D, bool PARTIAL>
-__global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     constexpr int RB = kRB;                   // 32-row query blocks per wave
@@ -372,13 +372,15 @@ __global__ __launch_bounds__(kThreads, kWavesPerSimd) void fa_fwd_kernel(FwdArgs
     // read; vwait() waits for them and names every destination.  Every read is one of two
     // per-lane base addresses (key rows +0 / +8, whose swizzles differ) plus an immediate:
     // lds_off(row + 32*b2 + 16*ss, ch + 4*db) = lds_off(row, ch) + (4*b2 + 2*ss)*8*ROWB + 512*db.
-    const unsigned vbase0 = (unsigned)(size_t)smem + lds_off<D>(tr_row, tr_col >> 3) + (tr_col & 7) * 2;
+    // (the V ring's base is in the address registers, keeping every immediate < 64 KiB)
+    const unsigned vbase0 =
+        (unsigned)(size_t)vring + lds_off<D>(tr_row, tr_col >> 3) + (tr_col & 7) * 2;
     const unsigned vbase1 =
-        (unsigned)(size_t)smem + lds_off<D>(tr_row + 8, tr_col >> 3) + (tr_col & 7) * 2 - 8 * ROWB;
+        (unsigned)(size_t)vring + lds_off<D>(tr_row + 8, tr_col >> 3) + (tr_col & 7) * 2 - 8 * ROWB;
     auto read_v = [](auto slot_c, auto i_c, u32x2 (&vf)[2][2], unsigned vbase0, unsigned vbase1) {
         constexpr int SLOT = decltype(slot_c)::value, I = decltype(i_c)::value;
         constexpr int B2 = I / NDB, DB = I % NDB;
-        constexpr int OFF = 2 * TILEB + SLOT * TILEB + 4 * B2 * 8 * ROWB + 512 * DB;
+        constexpr int OFF = SLOT * TILEB + 4 * B2 * 8 * ROWB + 512 * DB;
         constexpr int SSO = 2 * 8 * ROWB;  // +16 key rows (k-step ss = 1)
         static_assert(OFF + SSO + 8 * ROWB < 65536, "ds offset field is 16 bits");
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[0][0]) : "v"(vbase0), "i"(OFF) : "memory");
@@ -624,6 +626,7 @@ static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
         case 32: return launch_one<T, PT, 32, PARTIAL>(a, s);
         case 64: return launch_one<T, PT, 64, PARTIAL>(a, s);
         case 128: return launch_one<T, PT, 128, PARTIAL>(a, s);
+        case 256: return launch_one<T, PT, 256, PARTIAL>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -30,13 +30,20 @@ namespace fa {
 #ifndef FA_BK128
 #define FA_BK128 (FA_RB == 1 ? 64 : 32)
 #endif
-constexpr int bk_for(int d) { return d <= 32 ? FA_BK32 : d <= 64 ? FA_BK64 : FA_BK128; }
+#ifndef FA_BK256
+#define FA_BK256 32
+#endif
+constexpr int bk_for(int d) {
+    return d <= 32 ? FA_BK32 : d <= 64 ? FA_BK64 : d <= 128 ? FA_BK128 : FA_BK256;
+}
 constexpr int kRB = FA_RB;
 constexpr int kRowsPerWave = 32 * kRB;
 constexpr int kWaves = FA_WAVES;
 constexpr int kThreads = kWaves * 64;
 constexpr int kBQ = kWaves * kRowsPerWave;
 constexpr int kWavesPerSimd = kRB == 1 ? 2 : 1;  // occupancy the register budget is sized for
+// d = 256 holds 64 Q and 128 O registers per lane: one wave per SIMD, AGPRs in use
+constexpr int waves_per_simd(int d) { return d > 128 ? 1 : kWavesPerSimd; }
 
 enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2 };
 

@@ -22,7 +22,7 @@ from ._lib import FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP32, check, lib
 _DTYPES = {torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
 _PDTYPES = {torch.float32: FA_DTYPE_FP32, torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
 
-SUPPORTED_HEAD_DIMS = (32, 64, 128)
+SUPPORTED_HEAD_DIMS = (32, 64, 128, 256)
 
 
 def _stream(t):

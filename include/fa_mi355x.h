@@ -36,7 +36,7 @@
  *     element type is a runtime argument (FA_DTYPE_BF16 or FA_DTYPE_FP16);
  *   - the reference fixes the head dim at compile time (assert(d == D),
  *     flash_attention_v1/CUDA/flash_attention_v1.h:264); here d is dispatched at run
- *     time to kernels for d in {32, 64, 128}; any other d returns FA_ERR_UNSUPPORTED;
+ *     time to kernels for d in {32, 64, 128, 256}; any other d returns FA_ERR_UNSUPPORTED;
  *   - sizes are int64_t and every offset is 64-bit (the reference overflows int32 in
  *     its workspace index at L=4096, flash_attention_v2/CUDA/flash_attention_v2.h:324).
  */

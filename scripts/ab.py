@@ -13,7 +13,7 @@ import statistics
 import torch
 
 CFG = {"c2": (32, 8, 1024, 32), "c3": (32, 8, 1024, 128), "c3s": (32, 8, 4096, 128),
-       "c4": (32, 8, 4096, 128)}
+       "c4": (32, 8, 4096, 128), "d256": (32, 8, 1024, 256), "d64": (32, 8, 1024, 64)}
 
 
 def main():

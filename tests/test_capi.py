@@ -43,6 +43,8 @@ def test_version_and_geometry():
     bq, bk, threads, lds = L.geometry(128)
     assert (bq, bk, threads) == (128, 64, 256)
     assert lds == 2 * 2 * 64 * 128 * 2
+    bq, bk, threads, lds = L.geometry(256)  # one wave per SIMD, 32-key tiles
+    assert (bq, bk, threads, lds) == (128, 32, 256, 2 * 2 * 32 * 256 * 2)
     with pytest.raises(L.FaArgumentError):
         L.geometry(96)
 

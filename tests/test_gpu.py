@@ -161,7 +161,7 @@ SHAPES = [(1, 1, 1), (1, 2, 65), (2, 3, 200), (1, 2, 512)]
 
 @pytest.mark.parametrize("variant", ["v1", "tiled_d", "v2_kvtpb1_f32", "v2_kvtpb4_p16"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
-@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
 def test_matrix(gpu, variant, dtype, d):
     fn = _variants()[variant]
     for i, (B, H, L) in enumerate(SHAPES):
