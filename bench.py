@@ -208,7 +208,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
         # per-variant timings at N=1 (informational; not the headline value)
         for name, c, fn in (("c3_tiled_d", "c3", "tiled_d"), ("c2_fused", "c2", "v1"),
-                            ("c4_splitkv", "c4", "v2")):
+                            ("c4_splitkv", "c4", "v2"), ("c4_splitkv_auto", "c4", "v2auto")):
             cc = CONFIGS[c]
             qq, kk, vv = _make_inputs(torch, dev, cc["B"], cc["H"], cc["L"], cc["d"], seed=7)
             if fn == "tiled_d":
@@ -217,16 +217,19 @@ def main():
             elif fn == "v1":
                 def st():
                     ops.attention_v1(qq, kk, vv)
-            else:
-                nb, _ = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], 4, qq.dtype)
+            else:  # KV_TILES_PER_BLOCK = 4 as in C4, or the occupancy-chosen split
+                kvt = 4 if fn == "v2" else "auto"
+                nb, nsp = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
                 wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
 
                 def st():
-                    ops.attention_v2(qq, kk, vv, 4, workspace=wsx)
+                    ops.attention_v2(qq, kk, vv, kvt, workspace=wsx)
             n = 20
             _, ems = time_step(torch, st, n, 5, barrier)
             f = flops(cc["B"], cc["H"], cc["L"], cc["d"])
             extra[name] = {"ms": round(ems / n, 4), "tflops": round(f / (ems / n * 1e-3) / 1e12, 1)}
+            if fn.startswith("v2"):
+                extra[name]["splits"] = nsp
             del qq, kk, vv
 
     if rank == 0:

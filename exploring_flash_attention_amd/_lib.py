@@ -21,6 +21,8 @@ FA_DTYPE_FP16 = 0
 FA_DTYPE_BF16 = 1
 FA_DTYPE_FP32 = 2
 
+FA_KV_TILES_AUTO = -1  # kv_tiles_per_block: split chosen from the device's occupancy
+
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _I = ctypes.c_int

@@ -97,6 +97,52 @@ fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int6
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Split-KV workspace (fused split mode): normalised partial O [S][BH][nqt][BQ*d] (PT) and
+// lse [S][BH][nqt][BQ] (fp32), both in the kernel's fragment order, then one uint32
+// counter per (b*h, query tile).  Every part 256-byte aligned.
+struct V2Layout {
+    size_t o_bytes, lse_off, cnt_off, total;
+    int64_t ngroups;
+};
+V2Layout v2_layout(int64_t BH, int64_t L, int64_t d, int ns, fa::Elem pe) {
+    V2Layout w{};
+    const int64_t nqt = (L + fa::kBQ - 1) / fa::kBQ;
+    const size_t esz = pe == fa::Elem::F32 ? 4 : 2;
+    const size_t rows = (size_t)ns * BH * nqt * fa::kBQ;
+    w.ngroups = BH * nqt;
+    w.o_bytes = align256(rows * d * esz);
+    w.lse_off = w.o_bytes;
+    w.cnt_off = w.lse_off + align256(rows * sizeof(float));
+    w.total = w.cnt_off + align256((size_t)w.ngroups * sizeof(unsigned));
+    return w;
+}
+
+// Workgroups the device runs at once (forward kernel occupancy: 2 per CU, 1 at d = 256).
+int resident_workgroups(int64_t d) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) {
+        (void)hipGetLastError();
+        ncu = 256;  // MI355X
+    }
+    return ncu * fa::waves_per_simd((int)d);
+}
+
+// FA_KV_TILES_AUTO: pick the split from occupancy -- no split when the
+// query tiles alone fill the device twice over, else enough splits for about two
+// workgroups per slot (each split at least one KV tile).
+int auto_kv_tiles(int64_t BH, int64_t L, int64_t d) {
+    if (BH <= 0 || L <= 0 || !supported_d(d)) return 1;  // the shape checks report these
+    const int64_t bk = fa::bk_for((int)d);
+    const int64_t ntiles = (L + bk - 1) / bk;
+    const int64_t items = BH * ((L + fa::kBQ - 1) / fa::kBQ);
+    const int64_t want = 2 * (int64_t)resident_workgroups(d);
+    if (items >= want) return (int)ntiles;
+    int64_t ns = (want + items - 1) / items;
+    if (ns > ntiles) ns = ntiles;
+    return (int)((ntiles + ns - 1) / ns);
+}
+
 int splits_for(int64_t L, int64_t d, int kvtpb, int* kv_per_split) {
     const int64_t keys = (int64_t)kvtpb * fa::bk_for((int)d);
     *kv_per_split = (int)(keys < L ? keys : L);
@@ -130,7 +176,7 @@ int fa_fwd_v1(const void* q, const void* k, const void* v, void* o, int64_t B, i
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d);
-    if (hipError_t he = fa::launch_fwd(e, e, (int)d, false, a, (hipStream_t)stream))
+    if (hipError_t he = fa::launch_fwd(e, e, (int)d, fa::kFinal, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1 launch");
     return ok();
 }
@@ -143,7 +189,7 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o, int6
     if (int st = check_ptrs(q, k, v, o)) return st;
     if (int st = check_d_tiles(d, d_tile_qk, d_tile_v)) return st;
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d);
-    if (hipError_t he = fa::launch_fwd(e, e, (int)d, false, a, (hipStream_t)stream))
+    if (hipError_t he = fa::launch_fwd(e, e, (int)d, fa::kFinal, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1_tiled_d launch");
     return ok();
 }
@@ -154,14 +200,14 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
+    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d);
     if (kv_tiles_per_block <= 0)
         return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
     int kvps;
     const int ns = splits_for(L, d, kv_tiles_per_block, &kvps);
-    const size_t esz = pe == fa::Elem::F32 ? 4 : 2;
-    const size_t rows = (size_t)ns * B * H * L;
-    *bytes = align256(rows * d * esz) + align256(rows * sizeof(float));
+    const V2Layout w = v2_layout(B * H, L, d, ns, pe);
+    *bytes = w.total;
     if (num_splits) *num_splits = ns;
     return ok();
 }
@@ -172,6 +218,7 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
     fa::Elem e, pe;
     size_t need = 0;
     int ns = 0;
+    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d);
     if (int st = fa_fwd_v2_workspace_size(B, H, L, d, kv_tiles_per_block, dtype, partial_dtype,
                                           &need, &ns))
         return st;
@@ -185,25 +232,27 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
     if ((uintptr_t)workspace & 255) return fail(FA_ERR_WORKSPACE, "workspace must be 256-byte aligned");
 
     const int64_t BH = B * H;
-    const size_t esz = pe == fa::Elem::F32 ? 4 : 2;
-    const size_t rows = (size_t)ns * BH * L;
-    void* o_part = workspace;
-    float* lse = (float*)((char*)workspace + align256(rows * d * esz));
-
-    fa::FwdArgs a = base_args(q, k, v, o_part, BH, L, L, d);
+    fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d);
+    if (ns == 1) {  // one split: nothing to combine
+        if (hipError_t he = fa::launch_fwd(e, e, (int)d, fa::kFinal, a, (hipStream_t)stream))
+            return hip_fail(he, "fa_fwd_v2 launch");
+        return ok();
+    }
+    const V2Layout w = v2_layout(BH, L, d, ns, pe);
     int kvps;
     a.nsplit = splits_for(L, d, kv_tiles_per_block, &kvps);
     a.kv_per_split = kvps;
-    a.lse = lse;
-    a.chunk_rows = L;
-    a.split_stride = BH * L * d;
-    if (hipError_t he = fa::launch_fwd(e, pe, (int)d, true, a, (hipStream_t)stream))
-        return hip_fail(he, "fa_fwd_v2 partial launch");
-
-    fa::CombineArgs c{};
-    c.o_part = o_part; c.lse = lse; c.o = o; c.rows = BH * L; c.nsplit = ns;
-    if (hipError_t he = fa::launch_combine(e, pe, (int)d, c, (hipStream_t)stream))
-        return hip_fail(he, "fa_fwd_v2 combine launch");
+    a.o = workspace;
+    a.lse = (float*)((char*)workspace + w.lse_off);
+    a.counters = (unsigned*)((char*)workspace + w.cnt_off);
+    a.o_final = o;
+    // the kernel leaves every counter at zero; clearing them here makes a call that follows
+    // an aborted one (or a fresh workspace) safe
+    if (hipError_t he = hipMemsetAsync(a.counters, 0, (size_t)w.ngroups * sizeof(unsigned),
+                                       (hipStream_t)stream))
+        return hip_fail(he, "fa_fwd_v2 counter reset");
+    if (hipError_t he = fa::launch_fwd(e, pe, (int)d, fa::kFused, a, (hipStream_t)stream))
+        return hip_fail(he, "fa_fwd_v2 launch");
     return ok();
 }
 
@@ -225,7 +274,7 @@ int fa_fwd_partial(const void* q, const void* k, const void* v, void* o_part, fl
     a.lse = lse;
     a.chunk_rows = chunk_rows;
     a.split_stride = 0;
-    if (hipError_t he = fa::launch_fwd(e, pe, (int)d, true, a, (hipStream_t)stream))
+    if (hipError_t he = fa::launch_fwd(e, pe, (int)d, fa::kPartial, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_partial launch");
     return ok();
 }

@@ -1,12 +1,15 @@
 // fa_fwd.hip -- flash-attention forward for MI355X (gfx950 / CDNA4).
 //
 // One kernel template serves the three reference kernel families:
-//   final mode   (PARTIAL=false): FA-v1 fused / d-tiled forward
+//   final mode   (MODE=kFinal): FA-v1 fused / d-tiled forward
 //                 <- flash_attention_kernel    flash_attention_v1/CUDA/flash_attention_v1.h:161
 //                 <- flash_attention_kernel_opt1 flash_attention_v1/CUDA/flash_attention_v1_opt1.h:264
 //                 <- flash_attention_kernel (tiled-d) flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:230
-//   partial mode (PARTIAL=true): FA-v2 split-KV partial kernel
+//   partial mode (MODE=kPartial): FA-v2 split-KV partial kernel (+ fa_combine.hip)
 //                 <- partial_attention_kernel  flash_attention_v2/CUDA/flash_attention_v2.h:243
+//   fused split  (MODE=kFused): the same partials, combined by the last workgroup of each
+//                 query tile to finish (the reduction_kernel's maths,
+//                 flash_attention_v2/CUDA/flash_attention_v2.h:356, without its HBM pass)
 //
 // Online-softmax recurrence per KV tile (flash_attention_v1/numpy_gpu_like_opt2.py:135-195):
 //   S = Q K^T * scale; m_new = max(m, rowmax S); alpha = e^(m - m_new);
@@ -22,9 +25,9 @@
 //   * O^T = V^T . P^T: the S accumulator, exponentiated and packed to 16-bit, is already
 //     the B operand (no LDS round trip); V^T fragments come from ds_read_b64_tr_b16
 //     transposed LDS reads.  O_acc stays in VGPRs/AGPRs for the whole KV loop.
-//   * K and V tiles are register-staged (global_load_dwordx4 issued before the tile's
-//     MFMAs, ds_write_b128 after them) into a double-buffered, XOR-swizzled LDS image
-//     that is bank-conflict-free for both the row reads and the transposed reads.
+//   * K and V tiles go HBM -> LDS by LDS-DMA (buffer_load ... lds) into a double-buffered,
+//     XOR-swizzled LDS image that is bank-conflict-free for both the row reads and the
+//     transposed reads.
 //   * blockIdx is remapped so that all query tiles of one (b,h) land on one XCD and
 //     share that head's K/V in the XCD's L2.
 #include <utility>
@@ -166,7 +169,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds, int 
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
-template <typename T, typename PT, int D, bool PARTIAL>
+template <typename T, typename PT, int D, int MODE>
 __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
@@ -546,43 +549,177 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     }
 
     // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (i&3) + 8*(i>>2) + 4*hf
+    // store v * scale as one 16-bit output row (row base Oh)
+    auto store_row = [&](unsigned short* Oh, const f32x16 (&v)[NDB], float scale) {
+#if FA_WIDE_STORE
+        // Column groups g and g+1 of a row sit in lanes l (cols 8g..+3, 8g+8..+11) and
+        // l+32 (8g+4..+7, 8g+12..+15); one v_permlane32_swap per dword leaves 16
+        // contiguous bytes in each lane -> one dwordx4 store per pair instead of two
+        // dwordx2 (cdna_hip_programming.md T21).
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int gp = 0; gp < 4; gp += 2) {
+                unsigned x0 = pack2<T>(v[db][4 * gp + 0] * scale, v[db][4 * gp + 1] * scale);
+                unsigned x1 = pack2<T>(v[db][4 * gp + 2] * scale, v[db][4 * gp + 3] * scale);
+                unsigned y0 = pack2<T>(v[db][4 * gp + 4] * scale, v[db][4 * gp + 5] * scale);
+                unsigned y1 = pack2<T>(v[db][4 * gp + 6] * scale, v[db][4 * gp + 7] * scale);
+                const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+                const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+                const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
+                *(u32x4*)(Oh + db * 32 + 8 * gp + 8 * hf) = u;
+            }
+#else
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                u32x2 u;
+                u[0] = pack2<T>(v[db][4 * g4 + 0] * scale, v[db][4 * g4 + 1] * scale);
+                u[1] = pack2<T>(v[db][4 * g4 + 2] * scale, v[db][4 * g4 + 3] * scale);
+                *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
+            }
+#endif
+    };
+
+    if constexpr (MODE == kFused) {
+        // Split-KV partials combined on chip.  Every workgroup stores its normalised partial
+        // O (PT) and lse in FRAGMENT order -- lane-linear 16-byte pieces, so both the stores
+        // and the combine's loads are fully coalesced -- then counts itself in its query
+        // tile's counter; the workgroup that arrives last reads the other splits' partials
+        // (just written: served by L2 / Infinity Cache) and writes O.  Hand-off protocol
+        // (MI355X_MICROARCH.md, inter-workgroup visibility, first table row): all partial
+        // stores and loads sc1; every wave waits vmcnt(0) after its stores; a barrier; ONE
+        // lane's agent-scope atomic add; the adder that saw count nsplit-1 tells the other
+        // waves through LDS behind a barrier.  No workgroup ever waits for another.
+        constexpr int SC1 = 16;                    // cache-policy bit: sc1
+        constexpr int NF = NDB * 4;                // fragments (4 values) per lane and row block
+        constexpr int BLK = kBQ * D;               // partial elements per (split, tile) block
+        const int64_t grp = bh * a.nqt + qt;
+        auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
+        auto o_rsrc = [&](int sp) {
+            return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, (int64_t)BLK * sizeof(PT));
+        };
+        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
+        auto frag_off = [&](int r, int f) {  // byte offset of fragment f of row block r
+            return ((((wid * RB + r) * NF + f) * 64 + lane) * 4) * (int)sizeof(PT);
+        };
+        const int lse_off = (wid * RB) * 32 * 4 + l32 * 4;  // + r*128
+
+        float inv[RB], lse_own[RB];
+        {
+            const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
+                inv[r] = 1.f / l_tot;
+                lse_own[r] = m[r] + __builtin_amdgcn_logf(l_tot);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const int db = f >> 2, g4 = f & 3;
+                    const f32x4 src = {o[r][db][4 * g4], o[r][db][4 * g4 + 1], o[r][db][4 * g4 + 2],
+                                       o[r][db][4 * g4 + 3]};
+                    if constexpr (sizeof(PT) == 4) {
+                        const u32x4 u = {__float_as_uint(src[0] * inv[r]), __float_as_uint(src[1] * inv[r]),
+                                         __float_as_uint(src[2] * inv[r]), __float_as_uint(src[3] * inv[r])};
+                        __builtin_amdgcn_raw_buffer_store_b128(u, ors, frag_off(r, f), 0, SC1);
+                    } else {
+                        const u32x2 u = {pack2<T>(src[0] * inv[r], src[1] * inv[r]),
+                                         pack2<T>(src[2] * inv[r], src[3] * inv[r])};
+                        __builtin_amdgcn_raw_buffer_store_b64(u, ors, frag_off(r, f), 0, SC1);
+                    }
+                }
+                if (hf == 0)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse_own[r]), lrs, lse_off + r * 128, 0, SC1);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* const last_flag = (int*)smem;  // LDS is free: the KV loop ended with a barrier
+        if (tid == 0) {
+            const unsigned old = __hip_atomic_fetch_add(a.counters + grp, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old + 1 == (unsigned)a.nsplit;
+            if (last) a.counters[grp] = 0;  // leave the counter zero for the next launch
+            *last_flag = last;
+        }
+        __syncthreads();
+        if (!*last_flag) return;
+
+        // Sum in split order 0, 1, ... whatever workgroup came last (its own partial is read
+        // back too), so that O is bitwise repeatable.
+        const int ns = a.nsplit;
+        auto load_lse = [&](int sp, int r) {
+            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off + r * 128, 0, SC1));
+        };
+        typedef unsigned frag_t __attribute__((ext_vector_type(sizeof(PT))));  // 4 x PT
+        auto load_frags = [&](int sp, int r, frag_t (&dst)[NF]) {
+            const __amdgpu_buffer_rsrc_t rs = o_rsrc(sp);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                if constexpr (sizeof(PT) == 4)
+                    dst[f] = __builtin_bit_cast(frag_t, __builtin_amdgcn_raw_buffer_load_b128(rs, frag_off(r, f), 0, SC1));
+                else
+                    dst[f] = __builtin_bit_cast(frag_t, __builtin_amdgcn_raw_buffer_load_b64(rs, frag_off(r, f), 0, SC1));
+            }
+        };
+        auto unpack = [](const frag_t& u, int j) -> float {
+            if constexpr (sizeof(PT) == 4) {
+                return __uint_as_float(u[j]);
+            } else {
+                const unsigned w = u[j >> 1];
+                const unsigned short h = (unsigned short)((j & 1) ? (w >> 16) : (w & 0xffff));
+                return (float)__builtin_bit_cast(T, h);
+            }
+        };
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            float M = lse_own[r];
+            for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, load_lse(sp, r));
+            float wsum = 0.f;
+            f32x16 acc[NDB];
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) acc[db] = f32x16{};
+            auto fma_split = [&](const frag_t (&fr)[NF], float w) {
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[f >> 2][4 * (f & 3) + j] = __builtin_fmaf(w, unpack(fr[f], j), acc[f >> 2][4 * (f & 3) + j]);
+                wsum += w;
+            };
+            // two splits in flight: the loads of split sp+1 overlap the FMAs of split sp
+            frag_t fa_[NF], fb_[NF];
+            float wa, wb = 0.f;
+            load_frags(0, r, fa_);
+            wa = __builtin_amdgcn_exp2f(load_lse(0, r) - M);
+            for (int sp = 0; sp < ns; sp += 2) {
+                if (sp + 1 < ns) {
+                    load_frags(sp + 1, r, fb_);
+                    wb = __builtin_amdgcn_exp2f(load_lse(sp + 1, r) - M);
+                }
+                fma_split(fa_, wa);
+                if (sp + 1 < ns) {
+                    if (sp + 2 < ns) {
+                        load_frags(sp + 2, r, fa_);
+                        wa = __builtin_amdgcn_exp2f(load_lse(sp + 2, r) - M);
+                    }
+                    fma_split(fb_, wb);
+                }
+            }
+            const int64_t q_row = q_row0 + 32 * r;
+            if (q_row < a.Lq)
+                store_row((unsigned short*)a.o_final + bh * a.Lq * D + q_row * D, acc, 1.f / wsum);
+        }
+    } else {
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         const int64_t q_row = q_row0 + 32 * r;
         const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
         const float inv = 1.f / l_tot;
         if (q_row >= a.Lq) continue;
-        if constexpr (!PARTIAL) {
-            unsigned short* Oh = (unsigned short*)a.o + bh * a.Lq * D + q_row * D;
-#if FA_WIDE_STORE
-            // Column groups g and g+1 of a row sit in lanes l (cols 8g..+3, 8g+8..+11) and
-            // l+32 (8g+4..+7, 8g+12..+15); one v_permlane32_swap per dword leaves 16
-            // contiguous bytes in each lane -> one dwordx4 store per pair instead of two
-            // dwordx2 (cdna_hip_programming.md T21).
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                for (int gp = 0; gp < 4; gp += 2) {
-                    unsigned x0 = pack2<T>(o[r][db][4 * gp + 0] * inv, o[r][db][4 * gp + 1] * inv);
-                    unsigned x1 = pack2<T>(o[r][db][4 * gp + 2] * inv, o[r][db][4 * gp + 3] * inv);
-                    unsigned y0 = pack2<T>(o[r][db][4 * gp + 4] * inv, o[r][db][4 * gp + 5] * inv);
-                    unsigned y1 = pack2<T>(o[r][db][4 * gp + 6] * inv, o[r][db][4 * gp + 7] * inv);
-                    const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-                    const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-                    const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
-                    *(u32x4*)(Oh + db * 32 + 8 * gp + 8 * hf) = u;
-                }
-#else
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    u32x2 u;
-                    u[0] = pack2<T>(o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv);
-                    u[1] = pack2<T>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
-                    *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
-                }
-#endif
+        if constexpr (MODE == kFinal) {
+            store_row((unsigned short*)a.o + bh * a.Lq * D + q_row * D, o[r], inv);
         } else {
             const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
             const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
@@ -607,40 +744,47 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m[r] + __builtin_amdgcn_logf(l_tot);
         }
     }
+    }
 }
 
 int fwd_lds_bytes(int d) { return 2 * 2 * bk_for(d) * d * 2; }
 
-template <typename T, typename PT, int D, bool PARTIAL>
+template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
-    hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, PARTIAL>), dim3((unsigned)nblk), dim3(kThreads),
+    hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads),
                        lds, s, a);
     return hipGetLastError();
 }
 
-template <typename T, typename PT, bool PARTIAL>
+template <typename T, typename PT, int MODE>
 static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
     switch (d) {
-        case 32: return launch_one<T, PT, 32, PARTIAL>(a, s);
-        case 64: return launch_one<T, PT, 64, PARTIAL>(a, s);
-        case 128: return launch_one<T, PT, 128, PARTIAL>(a, s);
-        case 256: return launch_one<T, PT, 256, PARTIAL>(a, s);
+        case 32: return launch_one<T, PT, 32, MODE>(a, s);
+        case 64: return launch_one<T, PT, 64, MODE>(a, s);
+        case 128: return launch_one<T, PT, 128, MODE>(a, s);
+        case 256: return launch_one<T, PT, 256, MODE>(a, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_fwd(Elem t, Elem pt, int d, bool partial, const FwdArgs& a, hipStream_t s) {
-    if (!partial) {
-        if (t == Elem::BF16) return launch_d<__bf16, __bf16, false>(d, a, s);
-        if (t == Elem::F16) return launch_d<_Float16, _Float16, false>(d, a, s);
+hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s) {
+    if (mode == kFinal) {
+        if (t == Elem::BF16) return launch_d<__bf16, __bf16, kFinal>(d, a, s);
+        if (t == Elem::F16) return launch_d<_Float16, _Float16, kFinal>(d, a, s);
         return hipErrorInvalidValue;
     }
-    if (t == Elem::BF16 && pt == Elem::BF16) return launch_d<__bf16, __bf16, true>(d, a, s);
-    if (t == Elem::BF16 && pt == Elem::F32) return launch_d<__bf16, float, true>(d, a, s);
-    if (t == Elem::F16 && pt == Elem::F16) return launch_d<_Float16, _Float16, true>(d, a, s);
-    if (t == Elem::F16 && pt == Elem::F32) return launch_d<_Float16, float, true>(d, a, s);
+    auto pick = [&](auto mode_c) -> hipError_t {
+        constexpr int M = decltype(mode_c)::value;
+        if (t == Elem::BF16 && pt == Elem::BF16) return launch_d<__bf16, __bf16, M>(d, a, s);
+        if (t == Elem::BF16 && pt == Elem::F32) return launch_d<__bf16, float, M>(d, a, s);
+        if (t == Elem::F16 && pt == Elem::F16) return launch_d<_Float16, _Float16, M>(d, a, s);
+        if (t == Elem::F16 && pt == Elem::F32) return launch_d<_Float16, float, M>(d, a, s);
+        return hipErrorInvalidValue;
+    };
+    if (mode == kPartial) return pick(std::integral_constant<int, kPartial>{});
+    if (mode == kFused) return pick(std::integral_constant<int, kFused>{});
     return hipErrorInvalidValue;
 }
 

@@ -63,6 +63,17 @@ struct FwdArgs {
     int64_t chunk_rows;      // partial: output row chunking (divides Lq)
     int64_t split_stride;    // partial: elements between splits of o_part
     float scale_log2;        // log2(e) / sqrt(d)
+    // fused split mode only: the last workgroup of each (query tile, b*h) to finish combines
+    // the splits (see fa_fwd.hip); o / lse then hold the workspace in fragment order
+    unsigned* counters;      // [BH][nqt], zero before the launch; left zero after it
+    void* o_final;           // [BH][Lq][D] (T)
+};
+
+// Kernel modes: one workgroup per (query tile, split, b*h) in all three.
+enum Mode : int {
+    kFinal = 0,    // single split, writes O
+    kPartial = 1,  // writes normalised partial O + lse in row layout (fa_combine reads them)
+    kFused = 2,    // writes partials in fragment order; the last split to finish combines
 };
 
 struct CombineArgs {
@@ -74,7 +85,7 @@ struct CombineArgs {
 };
 
 // Launchers (defined in the .hip files).  Return hipSuccess or the launch error.
-hipError_t launch_fwd(Elem t, Elem pt, int d, bool partial, const FwdArgs& a, hipStream_t s);
+hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
 

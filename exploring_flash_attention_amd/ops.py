@@ -17,7 +17,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP32, check, lib
+from ._lib import FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP32, FA_KV_TILES_AUTO, check, lib
 
 _DTYPES = {torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
 _PDTYPES = {torch.float32: FA_DTYPE_FP32, torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
@@ -93,10 +93,15 @@ def attention_tiled_d(q, k, v, d_tile_qk=32, d_tile_v=32, out=None):
     return o
 
 
+def _kvtpb(kv_tiles_per_block):
+    return FA_KV_TILES_AUTO if kv_tiles_per_block == "auto" else int(kv_tiles_per_block)
+
+
 def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
                        partial_dtype=None):
     """(bytes, num_splits) of the split-KV workspace (partials fp32 unless partial_dtype)."""
     pd = torch.float32 if partial_dtype is None else partial_dtype
+    kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes = ctypes.c_size_t()
     ns = ctypes.c_int()
     check(lib().fa_fwd_v2_workspace_size(B, H, L, d, int(kv_tiles_per_block), _DTYPES[dtype],
@@ -108,7 +113,9 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
                  out=None, workspace=None):
     """FA-v2 split-KV forward (partial kernel + combine kernel).
 
-    A split is ``kv_tiles_per_block`` KV tiles of the kernel's own tile size (64 keys).
+    A split is ``kv_tiles_per_block`` KV tiles of the kernel's own tile size (64 keys;
+    32 at d = 256); ``kv_tiles_per_block="auto"`` lets the library pick the split from the
+    device's occupancy (no split when the query tiles already fill the GPU).
     Partial outputs are kept in fp32 by default (``partial_dtype=torch.bfloat16`` halves the
     workspace traffic at the cost of one extra 16-bit rounding of every partial).
     ``workspace`` (a uint8 device tensor) is allocated from torch's caching allocator when
@@ -118,6 +125,7 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
     o = _out(out, q)
     B, H, L, d = q.shape
     pd = torch.float32 if partial_dtype is None else partial_dtype
+    kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
     if workspace is None:
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=q.device)

@@ -92,6 +92,12 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o,
                       int d_tile_qk, int d_tile_v,
                       int dtype, void* stream);
 
+/* kv_tiles_per_block value that lets the library choose the split from the device's
+ * occupancy: no split when the query tiles fill the GPU, otherwise about two workgroups
+ * per resident slot (the reference's README presets, flash_attention_v2/README.md:29-32,
+ * made automatic). */
+#define FA_KV_TILES_AUTO (-1)
+
 /* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split is
  * kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
  * FA_DTYPE_FP32 or the input dtype.  *num_splits (may be NULL) receives the split count. */
@@ -99,9 +105,13 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d,
                              int kv_tiles_per_block, int dtype, int partial_dtype,
                              size_t* bytes, int* num_splits);
 
-/* FA-v2 split-KV forward: partial kernel over (q-tile, split, b*h), then the combine
- * kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
- * 256-byte aligned.  d_tile_qk / d_tile_v as for fa_fwd_v1_tiled_d. */
+/* FA-v2 split-KV forward: one workgroup per (q-tile, split, b*h) computes its split's
+ * normalised partial O and log-sum-exp into the workspace; the last workgroup of each
+ * q-tile to finish combines the splits with fa_combine's formula and writes O (the
+ * reduction kernel's maths without its separate pass over HBM).  One split: the plain
+ * FA-v1 kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
+ * 256-byte aligned, contents need not be initialised (a hipMemsetAsync of its counters
+ * precedes the launch on `stream`).  d_tile_qk / d_tile_v as for fa_fwd_v1_tiled_d. */
 int fa_fwd_v2(const void* q, const void* k, const void* v, void* o,
               int64_t B, int64_t H, int64_t L, int64_t d,
               int d_tile_qk, int d_tile_v, int kv_tiles_per_block,

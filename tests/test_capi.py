@@ -83,7 +83,8 @@ def test_workspace_size_and_v2_checks():
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
     rows = 16 * 32 * 8 * 4096
     assert ns.value == 16
-    assert nbytes.value == rows * 128 * 2 + rows * 4  # both parts already 256-aligned
+    # partial O + lse (fragment order, 128-row tiles: 4096 = 32 x 128) + one counter per tile
+    assert nbytes.value == rows * 128 * 2 + rows * 4 + 32 * 8 * 32 * 4
     assert nbytes.value > 2 ** 32  # 64-bit sizes (the reference overflows int32 here)
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
@@ -92,6 +93,13 @@ def test_workspace_size_and_v2_checks():
                                         ctypes.byref(nbytes), None) == L.FA_ERR_INVALID_ARG
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_BF16,
                                         ctypes.byref(nbytes), None) == L.FA_ERR_UNSUPPORTED
+    # automatic split (FA_KV_TILES_AUTO; no device here -> the MI355X's 256 CUs assumed)
+    assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, L.FA_KV_TILES_AUTO, L.FA_DTYPE_BF16,
+                                        L.FA_DTYPE_FP32, ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+    assert ns.value == 1  # 8192 query tiles already fill the device
+    assert lib.fa_fwd_v2_workspace_size(1, 1, 4096, 128, L.FA_KV_TILES_AUTO, L.FA_DTYPE_BF16,
+                                        L.FA_DTYPE_FP32, ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+    assert ns.value == 32  # 32 query tiles x 32 splits of 2 KV tiles ~ 2 per resident slot
     fake = ctypes.c_void_p(0x10000)
     st = lib.fa_fwd_v2(fake, fake, fake, fake, 1, 1, 100, 64, 32, 32, 1, fake, 16, L.FA_DTYPE_FP16,
                        L.FA_DTYPE_FP32, NULL)

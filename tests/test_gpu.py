@@ -326,3 +326,36 @@ def test_dist_single_rank_path_on_gpu(gpu):
     finally:
         if created:
             dist.destroy_process_group()
+
+
+def test_v2_fused_combine_repeatable(gpu):
+    """FA-v2's in-kernel combine (last workgroup of each query tile): bitwise repeatable,
+    independent of stale workspace contents, and equal to partial + separate combine."""
+    from exploring_flash_attention_amd import ops
+    q, k, v = (t.to(gpu) for t in _inputs(2, 3, 1000, 128, torch.bfloat16, seed=11))
+    nbytes, ns = ops.v2_workspace_bytes(2, 3, 1000, 128, 2)
+    assert ns == 8
+    ws = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=gpu)  # garbage counters
+    o1 = ops.attention_v2(q, k, v, 2, workspace=ws)
+    o2 = ops.attention_v2(q, k, v, 2, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    _gate(o1, _ref(q.cpu(), k.cpu(), v.cpu()), torch.bfloat16)
+    # the two-kernel form over the same 128-key splits, through fa_fwd_partial + fa_combine
+    parts = [ops.attention_partial(q, k[:, :, i:i + 128].contiguous(), v[:, :, i:i + 128].contiguous())
+             for i in range(0, 1000, 128)]
+    o_part = torch.cat([p[0] for p in parts])  # [S, BH, L, d]
+    lse = torch.cat([p[1] for p in parts])
+    o3 = ops.combine(o_part, lse, 2, 3, torch.bfloat16)
+    assert (o1.float() - o3.float()).abs().max().item() <= 2e-3
+
+
+def test_v2_auto_split(gpu):
+    from exploring_flash_attention_amd import ops
+    for (B, H, L) in ((1, 1, 4096), (1, 2, 700), (4, 8, 512)):
+        q, k, v = _inputs(B, H, L, 128, torch.bfloat16, seed=L)
+        _, ns = ops.v2_workspace_bytes(B, H, L, 128, "auto")
+        out = ops.attention_v2(q.to(gpu), k.to(gpu), v.to(gpu), "auto")
+        _gate(out, _ref(q, k, v), torch.bfloat16)
+        if B * H * ((L + 127) // 128) < 2 * 256:
+            assert ns > 1, (B, H, L, ns)
