@@ -20,6 +20,7 @@ FA_ERR_WORKSPACE = 4
 FA_DTYPE_FP16 = 0
 FA_DTYPE_BF16 = 1
 FA_DTYPE_FP32 = 2
+FA_DTYPE_FP64 = 3
 
 FA_KV_TILES_AUTO = -1  # kv_tiles_per_block: split chosen from the device's occupancy
 

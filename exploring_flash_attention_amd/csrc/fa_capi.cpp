@@ -38,10 +38,16 @@ bool supported_d(int64_t d) { return d == 32 || d == 64 || d == 128 || d == 256;
 int check_dtype(int dtype, fa::Elem* e) {
     if (dtype == FA_DTYPE_BF16) { *e = fa::Elem::BF16; return FA_OK; }
     if (dtype == FA_DTYPE_FP16) { *e = fa::Elem::F16; return FA_OK; }
-    return fail(FA_ERR_UNSUPPORTED, "dtype %d has no kernel (use FA_DTYPE_BF16 or FA_DTYPE_FP16)", dtype);
+    if (dtype == FA_DTYPE_FP64) { *e = fa::Elem::F64; return FA_OK; }
+    return fail(FA_ERR_UNSUPPORTED,
+                "dtype %d has no kernel (use FA_DTYPE_BF16, FA_DTYPE_FP16 or FA_DTYPE_FP64)", dtype);
 }
 
 int check_partial_dtype(int pdtype, int dtype, fa::Elem* e) {
+    if (dtype == FA_DTYPE_FP64) {
+        if (pdtype == FA_DTYPE_FP64) { *e = fa::Elem::F64; return FA_OK; }
+        return fail(FA_ERR_UNSUPPORTED, "fp64 inputs take fp64 partials (got partial dtype %d)", pdtype);
+    }
     if (pdtype == FA_DTYPE_FP32) { *e = fa::Elem::F32; return FA_OK; }
     if (pdtype == dtype) return check_dtype(dtype, e);
     return fail(FA_ERR_UNSUPPORTED, "partial dtype %d must be FA_DTYPE_FP32 or the input dtype %d",
@@ -81,18 +87,29 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(FA_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
+// query rows per workgroup and keys per KV tile of the kernel serving dtype e
+int rows_per_block(fa::Elem e) { return e == fa::Elem::F64 ? fa::fwd64_rows_per_block() : fa::kBQ; }
+int keys_per_tile(fa::Elem e, int64_t d) {
+    return e == fa::Elem::F64 ? fa::fwd64_keys_per_tile() : fa::bk_for((int)d);
+}
+
 fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int64_t BH,
-                      int64_t Lq, int64_t Lk, int64_t d) {
+                      int64_t Lq, int64_t Lk, int64_t d, fa::Elem e) {
     fa::FwdArgs a{};
     a.q = q; a.k = k; a.v = v; a.o = o; a.lse = nullptr;
     a.BH = BH; a.Lq = Lq; a.Lk = Lk;
-    a.nqt = (int)((Lq + fa::kBQ - 1) / fa::kBQ);
+    a.nqt = (int)((Lq + rows_per_block(e) - 1) / rows_per_block(e));
+    a.scale_log2_64 = 1.4426950408889634 / std::sqrt((double)d);
     a.nsplit = 1;
     a.kv_per_split = (int)Lk;
     a.chunk_rows = Lq;
     a.split_stride = 0;
     a.scale_log2 = (float)(1.4426950408889634 / std::sqrt((double)d));
     return a;
+}
+
+hipError_t launch_final(fa::Elem e, int d, const fa::FwdArgs& a, hipStream_t s) {
+    return e == fa::Elem::F64 ? fa::launch_fwd64(d, fa::kFinal, a, s) : fa::launch_fwd(e, e, d, fa::kFinal, a, s);
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -106,6 +123,14 @@ struct V2Layout {
 };
 V2Layout v2_layout(int64_t BH, int64_t L, int64_t d, int ns, fa::Elem pe) {
     V2Layout w{};
+    if (pe == fa::Elem::F64) {  // fp64: row-major partials + double lse, separate combine
+        const size_t rows = (size_t)ns * BH * L;
+        w.o_bytes = align256(rows * d * 8);
+        w.lse_off = w.o_bytes;
+        w.cnt_off = w.lse_off + align256(rows * 8);
+        w.total = w.cnt_off;
+        return w;
+    }
     const int64_t nqt = (L + fa::kBQ - 1) / fa::kBQ;
     const size_t esz = pe == fa::Elem::F32 ? 4 : 2;
     const size_t rows = (size_t)ns * BH * nqt * fa::kBQ;
@@ -131,11 +156,11 @@ int resident_workgroups(int64_t d) {
 // FA_KV_TILES_AUTO: pick the split from occupancy -- no split when the
 // query tiles alone fill the device twice over, else enough splits for about two
 // workgroups per slot (each split at least one KV tile).
-int auto_kv_tiles(int64_t BH, int64_t L, int64_t d) {
+int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
     if (BH <= 0 || L <= 0 || !supported_d(d)) return 1;  // the shape checks report these
-    const int64_t bk = fa::bk_for((int)d);
+    const int64_t bk = keys_per_tile(e, d);
     const int64_t ntiles = (L + bk - 1) / bk;
-    const int64_t items = BH * ((L + fa::kBQ - 1) / fa::kBQ);
+    const int64_t items = BH * ((L + rows_per_block(e) - 1) / rows_per_block(e));
     const int64_t want = 2 * (int64_t)resident_workgroups(d);
     if (items >= want) return (int)ntiles;
     int64_t ns = (want + items - 1) / items;
@@ -143,8 +168,8 @@ int auto_kv_tiles(int64_t BH, int64_t L, int64_t d) {
     return (int)((ntiles + ns - 1) / ns);
 }
 
-int splits_for(int64_t L, int64_t d, int kvtpb, int* kv_per_split) {
-    const int64_t keys = (int64_t)kvtpb * fa::bk_for((int)d);
+int splits_for(int64_t L, int64_t d, int kvtpb, int* kv_per_split, fa::Elem e) {
+    const int64_t keys = (int64_t)kvtpb * keys_per_tile(e, d);
     *kv_per_split = (int)(keys < L ? keys : L);
     return (int)((L + keys - 1) / keys);
 }
@@ -165,6 +190,12 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
     if (bq) *bq = fa::kBQ;
     if (bk) *bk = fa::bk_for((int)d);
     if (threads) *threads = fa::kThreads;
+    if (e == fa::Elem::F64) {  // fp64 mode: 64 rows x 16-key tiles, padded LDS rows
+        if (bq) *bq = fa::fwd64_rows_per_block();
+        if (bk) *bk = fa::fwd64_keys_per_tile();
+        if (lds_bytes) *lds_bytes = (int)(2 * 16 * (d + 1) * 8 + 4 * 16 * 17 * 8);
+        return ok();
+    }
     if (lds_bytes) *lds_bytes = fa::fwd_lds_bytes((int)d);
     return ok();
 }
@@ -175,8 +206,8 @@ int fa_fwd_v1(const void* q, const void* k, const void* v, void* o, int64_t B, i
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
-    fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d);
-    if (hipError_t he = fa::launch_fwd(e, e, (int)d, fa::kFinal, a, (hipStream_t)stream))
+    fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
+    if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1 launch");
     return ok();
 }
@@ -188,8 +219,8 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o, int6
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     if (int st = check_d_tiles(d, d_tile_qk, d_tile_v)) return st;
-    fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d);
-    if (hipError_t he = fa::launch_fwd(e, e, (int)d, fa::kFinal, a, (hipStream_t)stream))
+    fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
+    if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1_tiled_d launch");
     return ok();
 }
@@ -200,12 +231,12 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
-    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d);
+    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
     if (kv_tiles_per_block <= 0)
         return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
     int kvps;
-    const int ns = splits_for(L, d, kv_tiles_per_block, &kvps);
+    const int ns = splits_for(L, d, kv_tiles_per_block, &kvps, e);
     const V2Layout w = v2_layout(B * H, L, d, ns, pe);
     *bytes = w.total;
     if (num_splits) *num_splits = ns;
@@ -218,7 +249,8 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
     fa::Elem e, pe;
     size_t need = 0;
     int ns = 0;
-    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d);
+    if (kv_tiles_per_block == FA_KV_TILES_AUTO && check_dtype(dtype, &e) == FA_OK)
+        kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
     if (int st = fa_fwd_v2_workspace_size(B, H, L, d, kv_tiles_per_block, dtype, partial_dtype,
                                           &need, &ns))
         return st;
@@ -232,16 +264,29 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
     if ((uintptr_t)workspace & 255) return fail(FA_ERR_WORKSPACE, "workspace must be 256-byte aligned");
 
     const int64_t BH = B * H;
-    fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d);
+    fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d, e);
     if (ns == 1) {  // one split: nothing to combine
-        if (hipError_t he = fa::launch_fwd(e, e, (int)d, fa::kFinal, a, (hipStream_t)stream))
+        if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
             return hip_fail(he, "fa_fwd_v2 launch");
         return ok();
     }
     const V2Layout w = v2_layout(BH, L, d, ns, pe);
     int kvps;
-    a.nsplit = splits_for(L, d, kv_tiles_per_block, &kvps);
+    a.nsplit = splits_for(L, d, kv_tiles_per_block, &kvps, e);
     a.kv_per_split = kvps;
+    if (e == fa::Elem::F64) {  // fp64: the reference's two kernels (partial, then reduction)
+        a.o = workspace;
+        a.lse64 = (double*)((char*)workspace + w.lse_off);
+        a.chunk_rows = L;
+        a.split_stride = BH * L * d;
+        if (hipError_t he = fa::launch_fwd64((int)d, fa::kPartial, a, (hipStream_t)stream))
+            return hip_fail(he, "fa_fwd_v2 partial launch");
+        fa::CombineArgs c{};
+        c.o_part = workspace; c.lse64 = a.lse64; c.o = o; c.rows = BH * L; c.nsplit = ns;
+        if (hipError_t he = fa::launch_combine64((int)d, c, (hipStream_t)stream))
+            return hip_fail(he, "fa_fwd_v2 combine launch");
+        return ok();
+    }
     a.o = workspace;
     a.lse = (float*)((char*)workspace + w.lse_off);
     a.counters = (unsigned*)((char*)workspace + w.cnt_off);
@@ -256,7 +301,7 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
     return ok();
 }
 
-int fa_fwd_partial(const void* q, const void* k, const void* v, void* o_part, float* lse,
+int fa_fwd_partial(const void* q, const void* k, const void* v, void* o_part, void* lse,
                    int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d, int64_t chunk_rows,
                    int dtype, int partial_dtype, void* stream) {
     fa::Elem e, pe;
@@ -270,16 +315,19 @@ int fa_fwd_partial(const void* q, const void* k, const void* v, void* o_part, fl
     if (chunk_rows <= 0 || Lq % chunk_rows)
         return fail(FA_ERR_INVALID_ARG, "chunk_rows=%lld must divide Lq=%lld", (long long)chunk_rows,
                     (long long)Lq);
-    fa::FwdArgs a = base_args(q, k, v, o_part, B * H, Lq, Lk, d);
-    a.lse = lse;
+    fa::FwdArgs a = base_args(q, k, v, o_part, B * H, Lq, Lk, d, e);
+    a.lse = (float*)lse;
+    a.lse64 = (double*)lse;
     a.chunk_rows = chunk_rows;
     a.split_stride = 0;
-    if (hipError_t he = fa::launch_fwd(e, pe, (int)d, fa::kPartial, a, (hipStream_t)stream))
+    if (hipError_t he = e == fa::Elem::F64
+                            ? fa::launch_fwd64((int)d, fa::kPartial, a, (hipStream_t)stream)
+                            : fa::launch_fwd(e, pe, (int)d, fa::kPartial, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_partial launch");
     return ok();
 }
 
-int fa_combine(const void* o_part, const float* lse, void* o, int64_t num_splits, int64_t B,
+int fa_combine(const void* o_part, const void* lse, void* o, int64_t num_splits, int64_t B,
                int64_t H, int64_t L, int64_t d, int dtype, int partial_dtype, void* stream) {
     fa::Elem e, pe;
     if (int st = check_shape(B, H, L, d)) return st;
@@ -289,8 +337,10 @@ int fa_combine(const void* o_part, const float* lse, void* o, int64_t num_splits
     if (num_splits <= 0 || num_splits > 65536)
         return fail(FA_ERR_INVALID_ARG, "num_splits=%lld out of range", (long long)num_splits);
     fa::CombineArgs c{};
-    c.o_part = o_part; c.lse = lse; c.o = o; c.rows = B * H * L; c.nsplit = (int)num_splits;
-    if (hipError_t he = fa::launch_combine(e, pe, (int)d, c, (hipStream_t)stream))
+    c.o_part = o_part; c.lse = (const float*)lse; c.lse64 = (const double*)lse; c.o = o;
+    c.rows = B * H * L; c.nsplit = (int)num_splits;
+    if (hipError_t he = e == fa::Elem::F64 ? fa::launch_combine64((int)d, c, (hipStream_t)stream)
+                                           : fa::launch_combine(e, pe, (int)d, c, (hipStream_t)stream))
         return hip_fail(he, "fa_combine launch");
     return ok();
 }

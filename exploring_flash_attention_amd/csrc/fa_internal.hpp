@@ -45,7 +45,7 @@ constexpr int kWavesPerSimd = kRB == 1 ? 2 : 1;  // occupancy the register budge
 // d = 256 holds 64 Q and 128 O registers per lane: one wave per SIMD, AGPRs in use
 constexpr int waves_per_simd(int d) { return d > 128 ? 1 : kWavesPerSimd; }
 
-enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2 };
+enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2, F64 = 3 };
 
 // Arguments of the forward kernel (final and partial modes share one struct).
 struct FwdArgs {
@@ -67,6 +67,9 @@ struct FwdArgs {
     // the splits (see fa_fwd.hip); o / lse then hold the workspace in fragment order
     unsigned* counters;      // [BH][nqt], zero before the launch; left zero after it
     void* o_final;           // [BH][Lq][D] (T)
+    // fp64 mode (fa_fwd64.hip)
+    double scale_log2_64;    // log2(e) / sqrt(d) in double
+    double* lse64;           // partial only: log2-sum-exp per row (double)
 };
 
 // Kernel modes: one workgroup per (query tile, split, b*h) in all three.
@@ -82,11 +85,17 @@ struct CombineArgs {
     void* o;                 // [rows][D] (T)
     int64_t rows;            // BH * L
     int nsplit;
+    const double* lse64;     // fp64 mode: [nsplit][rows] (double)
 };
 
 // Launchers (defined in the .hip files).  Return hipSuccess or the launch error.
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
+// fp64 mode (fa_fwd64.hip): 64 query rows x 16-key tiles; final or row-layout partial
+hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);
+hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s);
+int fwd64_rows_per_block();
+int fwd64_keys_per_tile();
 
 }  // namespace fa

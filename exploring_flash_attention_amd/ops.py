@@ -17,10 +17,20 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP32, FA_KV_TILES_AUTO, check, lib
+from ._lib import (FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP32, FA_DTYPE_FP64, FA_KV_TILES_AUTO,
+                   check, lib)
 
-_DTYPES = {torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
-_PDTYPES = {torch.float32: FA_DTYPE_FP32, torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16}
+# torch.float64 runs the fp64 kernels (the reference's USE_FP64 build): fp64 MFMA, softmax,
+# partials and lse -- the bit-tight mode, not the fast one
+_DTYPES = {torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16, torch.float64: FA_DTYPE_FP64}
+_PDTYPES = {torch.float32: FA_DTYPE_FP32, torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16,
+            torch.float64: FA_DTYPE_FP64}
+
+
+def _default_pdtype(dtype, partial_dtype):
+    if partial_dtype is not None:
+        return partial_dtype
+    return torch.float64 if dtype == torch.float64 else torch.float32
 
 SUPPORTED_HEAD_DIMS = (32, 64, 128, 256)
 
@@ -52,7 +62,7 @@ def _check_tensor(name, t, dtype=None, device=None, ndim=4):
 def _check_qkv(q, k, v, same_len=True):
     _check_tensor("q", q)
     if q.dtype not in _DTYPES:
-        raise ValueError(f"q dtype {q.dtype} unsupported (bfloat16 or float16)")
+        raise ValueError(f"q dtype {q.dtype} unsupported (bfloat16, float16 or float64)")
     _check_tensor("k", k, q.dtype, q.device)
     _check_tensor("v", v, q.dtype, q.device)
     if k.shape != v.shape:
@@ -99,8 +109,9 @@ def _kvtpb(kv_tiles_per_block):
 
 def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
                        partial_dtype=None):
-    """(bytes, num_splits) of the split-KV workspace (partials fp32 unless partial_dtype)."""
-    pd = torch.float32 if partial_dtype is None else partial_dtype
+    """(bytes, num_splits) of the split-KV workspace (partials fp32 unless partial_dtype;
+    fp64 for fp64 inputs)."""
+    pd = _default_pdtype(dtype, partial_dtype)
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes = ctypes.c_size_t()
     ns = ctypes.c_int()
@@ -124,7 +135,7 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
     _check_qkv(q, k, v)
     o = _out(out, q)
     B, H, L, d = q.shape
-    pd = torch.float32 if partial_dtype is None else partial_dtype
+    pd = _default_pdtype(q.dtype, partial_dtype)
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
     if workspace is None:
@@ -138,12 +149,13 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
     return o
 
 
-def attention_partial(q, k, v, chunk_rows=None, partial_dtype=torch.float32, o_part=None, lse=None):
+def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None, lse=None):
     """Split-KV partial over one whole key range (k, v: [B, H, Lk, d]).
 
     Returns ``(o_part, lse)`` with o_part ``[Lq/chunk_rows, B*H, chunk_rows, d]`` holding the
     normalised partial output and lse ``[Lq/chunk_rows, B*H, chunk_rows]`` its base-2
-    log-sum-exp (of the scores times log2(e)/sqrt(d)).
+    log-sum-exp (of the scores times log2(e)/sqrt(d)); fp32 partials and lse by default,
+    fp64 for fp64 inputs.
     """
     _check_qkv(q, k, v, same_len=False)
     B, H, Lq, d = q.shape
@@ -152,8 +164,10 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=torch.float32, o_p
     if cr <= 0 or Lq % cr:
         raise ValueError(f"chunk_rows={cr} must divide Lq={Lq}")
     nch = Lq // cr
+    partial_dtype = _default_pdtype(q.dtype, partial_dtype)
+    lse_dtype = torch.float64 if q.dtype == torch.float64 else torch.float32
     o_part = _out(o_part, q, (nch, B * H, cr, d), partial_dtype)
-    lse = _out(lse, q, (nch, B * H, cr), torch.float32)
+    lse = _out(lse, q, (nch, B * H, cr), lse_dtype)
     check(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
                                cr, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
     return o_part, lse
@@ -162,7 +176,8 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=torch.float32, o_p
 def combine(o_part, lse, B, H, dtype, out=None):
     """Combine ``S`` partials o_part ``[S, B*H, L, d]`` / lse ``[S, B*H, L]`` -> ``[B, H, L, d]``."""
     _check_tensor("o_part", o_part, ndim=4)
-    _check_tensor("lse", lse, torch.float32, o_part.device, ndim=3)
+    _check_tensor("lse", lse, torch.float64 if o_part.dtype == torch.float64 else torch.float32,
+                  o_part.device, ndim=3)
     S, BH, L, d = o_part.shape
     if BH != B * H or tuple(lse.shape) != (S, BH, L):
         raise ValueError(f"inconsistent shapes o_part {tuple(o_part.shape)} lse {tuple(lse.shape)} "

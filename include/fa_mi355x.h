@@ -33,7 +33,7 @@
  *   - the reference launchers return void, assert() on bad arguments and end with
  *     cudaDeviceSynchronize(); these return a status and never synchronise;
  *   - the reference element type is __half (or double under USE_FP64); here the
- *     element type is a runtime argument (FA_DTYPE_BF16 or FA_DTYPE_FP16);
+ *     element type is a runtime argument (FA_DTYPE_BF16, FA_DTYPE_FP16 or FA_DTYPE_FP64);
  *   - the reference fixes the head dim at compile time (assert(d == D),
  *     flash_attention_v1/CUDA/flash_attention_v1.h:264); here d is dispatched at run
  *     time to kernels for d in {32, 64, 128, 256}; any other d returns FA_ERR_UNSUPPORTED;
@@ -61,7 +61,10 @@ typedef enum fa_status {
 typedef enum fa_dtype {
     FA_DTYPE_FP16 = 0,       /* IEEE binary16 storage, fp32 accumulate */
     FA_DTYPE_BF16 = 1,       /* bfloat16 storage, fp32 accumulate */
-    FA_DTYPE_FP32 = 2        /* only valid as the split-KV partial-output type */
+    FA_DTYPE_FP32 = 2,       /* only valid as the split-KV partial-output type */
+    FA_DTYPE_FP64 = 3        /* IEEE binary64 throughout (the reference's USE_FP64 build,
+                                flash_attention_v1/CUDA/flash_attention_v1.h:29-41): fp64
+                                MFMA, fp64 softmax, fp64 partials and lse */
 } fa_dtype_t;
 
 /* Library version, (major << 16) | (minor << 8) | patch. */
@@ -123,20 +126,20 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o,
  * Writes, for every query row, the normalised partial output and its log-sum-exp
  * (base 2, of the scaled scores: lse = log2(sum_j 2^(s_j * log2(e)/sqrt(d)))):
  *   o_part[(row / chunk_rows)][b*H + h][row % chunk_rows][:]   (partial_dtype)
- *   lse   [(row / chunk_rows)][b*H + h][row % chunk_rows]      (fp32)
+ *   lse   [(row / chunk_rows)][b*H + h][row % chunk_rows]      (fp32; fp64 for FP64)
  * chunk_rows must divide Lq.  chunk_rows = Lq gives a plain [B,H,Lq,d] layout;
  * chunk_rows = Lq / world gives the all-to-all send layout of the multi-GPU path. */
 int fa_fwd_partial(const void* q, const void* k, const void* v,
-                   void* o_part, float* lse,
+                   void* o_part, void* lse,
                    int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d,
                    int64_t chunk_rows, int dtype, int partial_dtype, void* stream);
 
 /* Combine num_splits partials: o_part [num_splits][B*H][L][d] (partial_dtype),
- * lse [num_splits][B*H][L] (fp32, base 2) -> o [B, H, L, d] (dtype), using
+ * lse [num_splits][B*H][L] (fp32, base 2; fp64 for FA_DTYPE_FP64) -> o [B, H, L, d] (dtype), using
  * O = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M), M = max_s lse_s
  * (the reference's formula, flash_attention_v2/numpy_gpu_like.py:269-288, on
  * normalised partials). */
-int fa_combine(const void* o_part, const float* lse, void* o,
+int fa_combine(const void* o_part, const void* lse, void* o,
                int64_t num_splits, int64_t B, int64_t H, int64_t L, int64_t d,
                int dtype, int partial_dtype, void* stream);
 

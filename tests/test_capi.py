@@ -43,6 +43,8 @@ def test_version_and_geometry():
     bq, bk, threads, lds = L.geometry(128)
     assert (bq, bk, threads) == (128, 64, 256)
     assert lds == 2 * 2 * 64 * 128 * 2
+    bq, bk, threads, lds = L.geometry(128, L.FA_DTYPE_FP64)  # fp64 mode: 64 rows x 16 keys
+    assert (bq, bk, threads) == (64, 16, 256)
     bq, bk, threads, lds = L.geometry(256)  # one wave per SIMD, 32-key tiles
     assert (bq, bk, threads, lds) == (128, 32, 256, 2 * 2 * 32 * 256 * 2)
     with pytest.raises(L.FaArgumentError):
@@ -92,6 +94,12 @@ def test_workspace_size_and_v2_checks():
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 0, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
                                         ctypes.byref(nbytes), None) == L.FA_ERR_INVALID_ARG
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_BF16,
+                                        ctypes.byref(nbytes), None) == L.FA_ERR_UNSUPPORTED
+    # fp64: 16-key tiles (KVTPB=4 -> 64-key splits, the reference's own), fp64 partials only
+    assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 4, L.FA_DTYPE_FP64, L.FA_DTYPE_FP64,
+                                        ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+    assert ns.value == 2 and nbytes.value == 2 * 100 * 64 * 8 + 2048  # + lse (1600 B -> 2048)
+    assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 4, L.FA_DTYPE_FP64, L.FA_DTYPE_FP32,
                                         ctypes.byref(nbytes), None) == L.FA_ERR_UNSUPPORTED
     # automatic split (FA_KV_TILES_AUTO; no device here -> the MI355X's 256 CUs assumed)
     assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, L.FA_KV_TILES_AUTO, L.FA_DTYPE_BF16,
