@@ -98,7 +98,7 @@ def test_workspace_size_and_v2_checks():
     # fp64: 16-key tiles (KVTPB=4 -> 64-key splits, the reference's own), fp64 partials only
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 4, L.FA_DTYPE_FP64, L.FA_DTYPE_FP64,
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
-    assert ns.value == 2 and nbytes.value == 2 * 100 * 64 * 8 + 2048  # + lse (1600 B -> 2048)
+    assert ns.value == 2 and nbytes.value == 2 * 100 * 64 * 8 + 1792  # + lse (1600 B, 256-aligned)
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 4, L.FA_DTYPE_FP64, L.FA_DTYPE_FP32,
                                         ctypes.byref(nbytes), None) == L.FA_ERR_UNSUPPORTED
     # automatic split (FA_KV_TILES_AUTO; no device here -> the MI355X's 256 CUs assumed)
