@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--mode", default="heads", choices=["heads", "splitkv-dist"])
+    ap.add_argument("--dist-impl", default="torch", choices=["torch", "native"],
+                    help="splitkv-dist exchange: torch.distributed all_to_all, or the C ABI "
+                         "fa_fwd_v2_dist (own RCCL communicator, grouped send/recv)")
     ap.add_argument("--cpu-heads", type=int, default=0, help="CPU baseline sample (0 = min(16, cores))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the per-variant extra timings")
@@ -177,7 +180,7 @@ def main():
 
             def step():
                 ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
-            kernel = "fa_fwd_kernel (partial) + fa_combine_kernel"
+            kernel = "fa_fwd_kernel (split-KV, in-kernel combine)"
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         work = flops(B, H, L, d)
         workload = f"FA-{'v1 fused' if cfg['variant'] == 'v1' else 'v2 split-KV'} forward"
@@ -188,11 +191,18 @@ def main():
         q, _, _ = _make_inputs(torch, dev, B, H, L, d, seed=99)  # same Q on every rank
         _, k, v = _make_inputs(torch, dev, B, H, 1, d, seed=1000 + rank, Lk=hi - lo)
 
-        def step():
-            fdist.splitkv_attention(q, k, v)
+        if args.dist_impl == "native":
+            comm = fdist.RcclComm()
+
+            def step():
+                fdist.splitkv_attention_native(q, k, v, comm)
+            kernel = "fa_fwd_kernel (partial) + RCCL send/recv + fa_combine_kernel (C ABI)"
+        else:
+            def step():
+                fdist.splitkv_attention(q, k, v)
+            kernel = "fa_fwd_kernel (partial) + all_to_all + fa_combine_kernel"
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         work = flops(B, H, L, d, Lk=hi - lo)  # this rank's share
-        kernel = "fa_fwd_kernel (partial) + all_to_all + fa_combine_kernel"
         workload = "FA-v2 split-KV forward, keys sharded over ranks"
         parallel = f"kv{world}"
 

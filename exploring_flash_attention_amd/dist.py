@@ -49,7 +49,7 @@ def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=torch.bfloa
     [B, H, L/W, d].  Returns this rank's query rows [B, H, L/W, d] of O, or the full
     [B, H, L, d] O when ``gather``.
     """
-    world = dist.get_world_size(group)
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     B, H, L, d = q.shape
     if L % world:
         raise ValueError(f"L={L} must be divisible by world size {world}")
@@ -70,3 +70,111 @@ def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=torch.bfloa
     parts = [torch.empty_like(o_local) for _ in range(world)]
     dist.all_gather(parts, o_local.contiguous(), group=group)
     return torch.cat(parts, dim=2)
+
+
+# ----------------------------------------------------------------------------------------
+# the same forward through the native C ABI (include/fa_mi355x_dist.h): one RCCL
+# communicator owned by libfa_mi355x_dist.so, the whole sequence issued from C++
+# ----------------------------------------------------------------------------------------
+
+_dist_lib = None
+
+
+def dist_lib():
+    """ctypes handle of libfa_mi355x_dist.so (loaded on first use; raises if not built)."""
+    global _dist_lib
+    if _dist_lib is None:
+        import ctypes
+        import os
+
+        from . import _lib
+        path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libfa_mi355x_dist.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: build it with `python __graft_entry__.py`")
+        _lib.lib()  # the core library first (the dist library links it)
+        h = ctypes.CDLL(path)
+        P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        for name, res, args in (
+                ("fa_dist_last_error", ctypes.c_char_p, []),
+                ("fa_dist_get_unique_id", I, [P]),
+                ("fa_dist_comm_init", I, [ctypes.POINTER(P), I, I, P]),
+                ("fa_dist_comm_destroy", I, [P]),
+                ("fa_fwd_v2_dist_workspace_size", I, [I64, I64, I64, I64, I, I, I,
+                                                      ctypes.POINTER(ctypes.c_size_t)]),
+                ("fa_fwd_v2_dist", I, [P, P, P, P, I64, I64, I64, I64, P, I, P, ctypes.c_size_t,
+                                       I, I, P])):
+            fn = getattr(h, name)
+            fn.restype, fn.argtypes = res, args
+        _dist_lib = h
+    return _dist_lib
+
+
+def _dcheck(st):
+    if st:
+        from ._lib import FaError
+        raise FaError(st, dist_lib().fa_dist_last_error().decode())
+
+
+class RcclComm:
+    """An RCCL communicator of libfa_mi355x_dist.so over the ranks of ``group``.
+
+    The 128-byte RCCL id is created on rank 0 and broadcast with torch.distributed (any
+    backend); with no process group initialised the communicator has one rank.
+    """
+
+    def __init__(self, group=None):
+        import ctypes
+        lib = dist_lib()
+        if dist.is_available() and dist.is_initialized():
+            self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        else:
+            self.world, self.rank = 1, 0
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            _dcheck(lib.fa_dist_get_unique_id(uid))
+        if self.world > 1:
+            box = [bytes(uid.raw)]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group else 0, group=group)
+            uid = ctypes.create_string_buffer(box[0], 128)
+        self._comm = ctypes.c_void_p()
+        _dcheck(lib.fa_dist_comm_init(ctypes.byref(self._comm), self.world, self.rank, uid))
+
+    @property
+    def handle(self):
+        return self._comm
+
+    def close(self):
+        if self._comm:
+            _dcheck(dist_lib().fa_dist_comm_destroy(self._comm))
+            self._comm = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def splitkv_attention_native(q, k_shard, v_shard, comm, gather=False, partial_dtype=None,
+                             workspace=None):
+    """``splitkv_attention`` through the C ABI (fa_fwd_v2_dist): partial kernel, one grouped
+    RCCL send/recv round, combine kernel (and all-gather), all on the current stream."""
+    import ctypes
+    ops._check_qkv(q, k_shard, v_shard, same_len=False)
+    B, H, L, d = q.shape
+    W = comm.world
+    if L % W or k_shard.shape[2] * W != L:
+        raise ValueError(f"L={L} must be divisible by world {W} and k_shard must hold L/W keys")
+    # 16-bit partials by default, as splitkv_attention: they halve the exchanged bytes
+    pd = q.dtype if partial_dtype is None else partial_dtype
+    nbytes = ctypes.c_size_t()
+    _dcheck(dist_lib().fa_fwd_v2_dist_workspace_size(B, H, L, d, W, ops._DTYPES[q.dtype],
+                                                     ops._PDTYPES[pd], ctypes.byref(nbytes)))
+    if workspace is None:
+        workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=q.device)
+    out = torch.empty((B, H, L if gather else L // W, d), dtype=q.dtype, device=q.device)
+    _dcheck(dist_lib().fa_fwd_v2_dist(ops._ptr(q), ops._ptr(k_shard), ops._ptr(v_shard), ops._ptr(out),
+                                      B, H, L, d, comm.handle, int(bool(gather)), ops._ptr(workspace),
+                                      workspace.numel(), ops._DTYPES[q.dtype], ops._PDTYPES[pd],
+                                      ops._stream(q)))
+    return out

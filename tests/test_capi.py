@@ -144,3 +144,26 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         L.lib()
+
+
+def test_dist_library_exports():
+    """libfa_mi355x_dist.so (RCCL path) exports every function of include/fa_mi355x_dist.h."""
+    import ctypes
+    path = os.path.join(os.path.dirname(L.LIB_PATH), "libfa_mi355x_dist.so")
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "fa_mi355x_dist.h")).read()
+    names = re.findall(r"^(?:int|const char\*)\s+(fa_\w+)\(", hdr, flags=re.M)
+    assert len(names) == 6, names
+    out = os.popen(f"nm -D --defined-only {path}").read()
+    for name in names:
+        assert re.search(rf"\bT {name}$", out, flags=re.M), name
+    from exploring_flash_attention_amd import dist as fadist
+    lib = fadist.dist_lib()
+    nbytes = ctypes.c_size_t()
+    assert lib.fa_fwd_v2_dist_workspace_size(2, 2, 100, 64, 3, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                             ctypes.byref(nbytes)) == L.FA_ERR_INVALID_ARG  # 100 % 3
+    assert b"divisible" in lib.fa_dist_last_error()
+    assert lib.fa_fwd_v2_dist_workspace_size(2, 2, 96, 64, 4, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                             ctypes.byref(nbytes)) == 0
+    rows = 4 * 96
+    assert nbytes.value == 2 * (rows * 64 * 4 + rows * 4) + rows * 64 * 2
+

@@ -332,6 +332,25 @@ def test_dist_single_rank_path_on_gpu(gpu):
             dist.destroy_process_group()
 
 
+def test_dist_native_rccl_single_rank(gpu):
+    """fa_fwd_v2_dist (C ABI, RCCL communicator of libfa_mi355x_dist.so) at world size 1:
+    partial -> (no exchange) -> combine, rows and gathered forms, bf16 and fp64."""
+    from exploring_flash_attention_amd import dist as fdist
+    comm = fdist.RcclComm()
+    try:
+        assert comm.world == 1
+        q, k, v = _inputs(1, 2, 384, 128, torch.bfloat16, seed=8)
+        ref = _ref(q, k, v)
+        for gather in (False, True):
+            o = fdist.splitkv_attention_native(q.to(gpu), k.to(gpu), v.to(gpu), comm, gather=gather)
+            torch.cuda.synchronize()
+            _gate(o, ref, torch.bfloat16)
+        q, k, v = _inputs(1, 2, 100, 64, torch.float64, seed=9)
+        o = fdist.splitkv_attention_native(q.to(gpu), k.to(gpu), v.to(gpu), comm, gather=True)
+        assert np.abs(o.cpu().numpy() - _ref(q, k, v)).max() <= 1e-12
+    finally:
+        comm.close()
+
 def test_v2_fused_combine_repeatable(gpu):
     """FA-v2's in-kernel combine (last workgroup of each query tile): bitwise repeatable,
     independent of stale workspace contents, and equal to partial + separate combine."""
