@@ -73,6 +73,12 @@
 #ifndef FA_ABL_NOQK
 #define FA_ABL_NOQK 0
 #endif
+#ifndef FA_UNIFORM_WID
+#define FA_UNIFORM_WID 0  // readfirstlane wave id: -2 % at d=128 (A/B), neutral at d=32/64
+#endif
+#ifndef FA_RSRC32
+#define FA_RSRC32 1
+#endif
 #ifndef FA_QK_LEAD
 #define FA_QK_LEAD 4
 #endif
@@ -150,6 +156,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
                                              0x00020000);
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc32(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
 // Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N), so that each
 // body can feed i into an inline-asm "i" (immediate) operand.
 template <typename F, int... I>
@@ -200,7 +210,13 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    // wave-uniform and PROVABLY so (an SGPR): the LDS-DMA destinations (M0) derived from it
+    // then need no v_readfirstlane per DMA, and no VGPRs hold per-piece LDS addresses
+#if FA_UNIFORM_WID
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+#else
     const int wid = tid >> 6;
+#endif
     const int l32 = lane & 31;
     const int hf = lane >> 5;
 
@@ -218,7 +234,6 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     // does not rely on soffset -- zero-fills the rows of a partial last tile.
     const unsigned short* const kbase = (const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D;
     const unsigned short* const vbase = (const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D;
-    const int64_t kv_bytes = (int64_t)nkv * ROWB;
 
     // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7] of each of its
     // RB row blocks.  Rows past Lq read zeros and are never stored.
@@ -250,9 +265,19 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         dma_src[i] = row * ROWB + ch * 16;
     }
     auto dma_tile = [&](const unsigned short* base, char* slot, int t) {
+        // descriptor over exactly the tile's valid keys (32-bit scalar arithmetic)
+        // (readfirstlane: hipcc evaluates the clamp with v_med3, and a descriptor word it
+        // cannot prove uniform turns every buffer op into a waterfall loop -- T20)
+#if FA_RSRC32
+        const int rem = nkv - t * kBK;
+        const int valid = __builtin_amdgcn_readfirstlane(rem < kBK ? (rem > 0 ? rem : 0) : kBK);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc32((const char*)base + (int64_t)t * TILEB, valid * ROWB);
+#else
         const int64_t off = (int64_t)t * TILEB;
+        const int64_t kv_bytes = (int64_t)nkv * ROWB;
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc((const char*)base + off, kv_bytes > off ? kv_bytes - off : 0);
+#endif
         if (NDMA >= kWaves || dma_wave) {
 #pragma unroll
             for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], 0);
