@@ -212,6 +212,19 @@ int fa_fwd_v1(const void* q, const void* k, const void* v, void* o, int64_t B, i
     return ok();
 }
 
+int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
+                  int64_t L, int64_t d, int dtype, void* stream) {
+    fa::Elem e;
+    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_dtype(dtype, &e)) return st;
+    if (int st = check_ptrs(q, k, v, o)) return st;
+    if (d != 128 || e == fa::Elem::F64)
+        return fail(FA_ERR_UNSUPPORTED, "the 64-row-wave kernel serves d=128 bf16/fp16 only");
+    fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
+    if (hipError_t he = fa::launch_fwd_w64(e, a, (hipStream_t)stream)) return hip_fail(he, "fa_fwd_v1_w64 launch");
+    return ok();
+}
+
 int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
                       int64_t L, int64_t d, int d_tile_qk, int d_tile_v, int dtype, void* stream) {
     fa::Elem e;

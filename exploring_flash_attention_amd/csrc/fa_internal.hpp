@@ -92,6 +92,12 @@ struct CombineArgs {
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
+// d = 128 final mode with 64 rows per wave (fa_fwd_w64.hip); FA_W64 selects it
+#ifndef FA_W64
+#define FA_W64 0  // measured: steady state equal to fa_fwd_kernel, per-item seam 1.5x
+#endif
+hipError_t launch_fwd_w64(Elem t, const FwdArgs& a, hipStream_t s);
+int w64_rows_per_block();
 // fp64 mode (fa_fwd64.hip): 64 query rows x 16-key tiles; final or row-layout partial
 hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s);

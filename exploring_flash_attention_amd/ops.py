@@ -93,6 +93,15 @@ def attention_v1(q, k, v, out=None):
     return o
 
 
+def attention_v1_w64(q, k, v, out=None):
+    """FA-v1 forward on the experimental 64-rows-per-wave kernel (d = 128 only)."""
+    _check_qkv(q, k, v)
+    o = _out(out, q)
+    B, H, L, d = q.shape
+    check(lib().fa_fwd_v1_w64(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
+    return o
+
+
 def attention_tiled_d(q, k, v, d_tile_qk=32, d_tile_v=32, out=None):
     """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher."""
     _check_qkv(q, k, v)

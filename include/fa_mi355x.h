@@ -101,6 +101,13 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o,
  * made automatic). */
 #define FA_KV_TILES_AUTO (-1)
 
+/* Experimental: the FA-v1 forward at d = 128 (bf16 / fp16) on the 64-rows-per-wave kernel
+ * (csrc/fa_fwd_w64.hip: one wave per SIMD, MFMA state in asm-owned AGPRs, persistent
+ * workgroups).  Same arguments and results as fa_fwd_v1; kept for measurement
+ * ("64-row waves"): fa_fwd_v1 uses it only when built with -DFA_W64=1. */
+int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o,
+                  int64_t B, int64_t H, int64_t L, int64_t d, int dtype, void* stream);
+
 /* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split is
  * kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
  * FA_DTYPE_FP32 or the input dtype.  *num_splits (may be NULL) receives the split count. */

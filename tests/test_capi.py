@@ -167,3 +167,12 @@ def test_dist_library_exports():
     rows = 4 * 96
     assert nbytes.value == 2 * (rows * 64 * 4 + rows * 4) + rows * 64 * 2
 
+
+def test_w64_asm_hazard_check():
+    """The inline-asm MFMA kernel passes the static ISA checks (scripts/check_asm_mfma.py)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "..", "scripts",
+                                                     "check_asm_mfma.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
