@@ -71,9 +71,17 @@
 #ifndef FA_ABL_NOQK
 #define FA_ABL_NOQK 0
 #endif
+// readfirstlane wave id (the DMA's M0 values become SGPR arithmetic): a bitmask over
+// d = 32/64/128/256 (bits 0..3).  A/B with the no-tail step: d=32 +3 %, d=64 0, d=128 -1.7 %.
 #ifndef FA_UNIFORM_WID
-#define FA_UNIFORM_WID 0  // readfirstlane wave id: -2 % at d=128 (A/B), neutral at d=32/64
+#define FA_UNIFORM_WID 1
 #endif
+// the no-tail specialisation (TAIL = false) per d, same bitmask: d=32 +1.6 %, d=128 +0.5 %,
+// d=64 -7 % (hipcc's schedule of the single-block step is worse there)
+#ifndef FA_NOTAIL_MASK
+#define FA_NOTAIL_MASK 0xD
+#endif
+constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
 #ifndef FA_RSRC32
 #define FA_RSRC32 1
 #endif
@@ -83,7 +91,10 @@
 
 namespace fa {
 
-template <typename T, typename PT, int D, int MODE>
+// TAIL: Lk is not a multiple of the KV tile, so the last tile of a split is partial (key
+// mask, clamped DMA descriptor).  Without it the steady-state step has no mask branch, which
+// would otherwise split the step into basic blocks and push the row sums out of the MFMA block.
+template <typename T, typename PT, int D, int MODE, bool TAIL>
 __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
@@ -116,11 +127,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     const int lane = tid & 63;
     // wave-uniform and PROVABLY so (an SGPR): the LDS-DMA destinations (M0) derived from it
     // then need no v_readfirstlane per DMA, and no VGPRs hold per-piece LDS addresses
-#if FA_UNIFORM_WID
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-#else
-    const int wid = tid >> 6;
-#endif
+    const int wid = (FA_UNIFORM_WID & d_bit(D)) ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int l32 = lane & 31;
     const int hf = lane >> 5;
 
@@ -174,7 +181,8 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         // cannot prove uniform turns every buffer op into a waterfall loop -- T20)
 #if FA_RSRC32
         const int rem = nkv - t * kBK;
-        const int valid = __builtin_amdgcn_readfirstlane(rem < kBK ? (rem > 0 ? rem : 0) : kBK);
+        const int valid = TAIL ? __builtin_amdgcn_readfirstlane(rem < kBK ? (rem > 0 ? rem : 0) : kBK)
+                               : (t < ntiles ? kBK : 0);
         const __amdgpu_buffer_rsrc_t rs = make_rsrc32((const char*)base + (int64_t)t * TILEB, valid * ROWB);
 #else
         const int64_t off = (int64_t)t * TILEB;
@@ -341,7 +349,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         //   MASKNEXT  tile t+1 may be the partial last tile (needs the key mask)
         //   DMAK      tile t+2 exists (its K is prefetched now)
         constexpr int F = decltype(flags_c)::value;
-        constexpr bool MORE = F & 1, MASKNEXT = F & 2, DMAK = F & 4;
+        constexpr bool MORE = F & 1, MASKNEXT = TAIL && (F & 2), DMAK = F & 4;
 #if !FA_DMA_LATE
         if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(kbase, kring + P * TILEB, t + 2);
         if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
@@ -449,7 +457,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     f32x16 sa[RB][NKB], sb[RB][NKB];
     float mx[RB];
     qk(kring, sa);
-    mask(0, sa);
+    if constexpr (TAIL) mask(0, sa);
     rowmax(sa, mx);
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
 
@@ -682,8 +690,12 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
-    hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads),
-                       lds, s, a);
+    if (a.Lk % bk_for(D) || !(FA_NOTAIL_MASK & d_bit(D)))
+        hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads),
+                           lds, s, a);
+    else
+        hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, false>), dim3((unsigned)nblk), dim3(kThreads),
+                           lds, s, a);
     return hipGetLastError();
 }
 
