@@ -89,6 +89,34 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 #define FA_QK_LEAD 4
 #endif
 
+// FA_STAMPS (diagnostic builds only): wave 0 of every workgroup writes s_memtime stamps at
+// the phase boundaries into g_fa_stamps (never into an output), read back through
+// fa_debug_stamps() by scripts/stamps.py.  Slots per workgroup: 0 entry, 1 Q/K0/V0/K1
+// landed, 2 loop start, 3 loop end, 4 stores issued, 5 stores retired, 6 hw_id, 7 xcc_id,
+// 8 / 9 s_memrealtime (100 MHz, one time base for all CUs) at entry / after the stores retired.
+#ifndef FA_STAMPS
+#define FA_STAMPS 0
+#endif
+#if FA_STAMPS
+#define FA_MAX_STAMP_WG 65536
+__device__ unsigned long long g_fa_stamps[FA_MAX_STAMP_WG * 16];
+#define FA_STAMP_V(i, v)                                                                       \
+    do {                                                                                       \
+        if (tid == 0 && blockIdx.x < FA_MAX_STAMP_WG)                                          \
+            __hip_atomic_store(&g_fa_stamps[blockIdx.x * 16 + (i)], (unsigned long long)(v),     \
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     \
+    } while (0)
+#define FA_STAMP(i) FA_STAMP_V(i, __builtin_amdgcn_s_memtime())
+extern "C" int fa_debug_stamps(void* dst, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fa_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define FA_STAMP_V(i, v) \
+    do {                 \
+    } while (0)
+#define FA_STAMP(i) FA_STAMP_V(i, 0)
+#endif
+
 namespace fa {
 
 // TAIL: Lk is not a multiple of the KV tile, so the last tile of a split is partial (key
@@ -131,6 +159,10 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     const int l32 = lane & 31;
     const int hf = lane >> 5;
 
+    FA_STAMP_V(8, __builtin_amdgcn_s_memrealtime());
+    FA_STAMP(0);
+    FA_STAMP_V(6, __builtin_amdgcn_s_getreg(4 | (31 << 11)));   // HW_REG_HW_ID, 32 bits
+    FA_STAMP_V(7, __builtin_amdgcn_s_getreg(20 | (31 << 11)));  // HW_REG_XCC_ID
     const int64_t kv_begin = (int64_t)split * a.kv_per_split;
     const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
     const int nkv = (int)(kv_end - kv_begin);
@@ -454,12 +486,14 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[r][ks]));
     __syncthreads();
+    FA_STAMP(1);
     f32x16 sa[RB][NKB], sb[RB][NKB];
     float mx[RB];
     qk(kring, sa);
     if constexpr (TAIL) mask(0, sa);
     rowmax(sa, mx);
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
+    FA_STAMP(2);
 
     {
         using C0 = std::integral_constant<int, 0>;
@@ -485,6 +519,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         }
     }
 
+    FA_STAMP(3);
     // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (i&3) + 8*(i>>2) + 4*hf
     // store v * scale as one 16-bit output row (row base Oh)
     auto store_row = [&](unsigned short* Oh, const f32x16 (&v)[NDB], float scale) {
@@ -682,6 +717,12 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         }
     }
     }
+#if FA_STAMPS
+    FA_STAMP(4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FA_STAMP(5);
+    FA_STAMP_V(9, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 int fwd_lds_bytes(int d) { return 2 * 2 * bk_for(d) * d * 2; }
@@ -712,6 +753,7 @@ static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
 
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s) {
     if (FA_W64 && mode == kFinal && d == 128) return launch_fwd_w64(t, a, s);
+    if (FA_PERSIST && mode == kFinal && d <= 128) return launch_fwd_persist(t, d, a, s);
     if (mode == kFinal) {
         if (t == Elem::BF16) return launch_d<__bf16, __bf16, kFinal>(d, a, s);
         if (t == Elem::F16) return launch_d<_Float16, _Float16, kFinal>(d, a, s);
