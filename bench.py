@@ -109,6 +109,27 @@ def time_step(torch, step, steps, warmup, barrier):
     return wall, ev0.elapsed_time(ev1)
 
 
+def c5_step(torch, fdist, dev, world, rank, impl="torch"):
+    """One C5 split-KV step closure: the keys of B=32 H=8 L=16384 d=128 sharded over the
+    ranks, partial kernel -> all-to-all -> combine (dist.splitkv_attention)."""
+    cc = CONFIGS["c5"]
+    B, H, L, d = cc["B"], cc["H"], cc["L"], cc["d"]
+    lo, hi = fdist.shard_bounds(L, world, rank)
+    q, _, _ = _make_inputs(torch, dev, B, H, L, d, seed=99)  # same Q on every rank
+    _, k, v = _make_inputs(torch, dev, B, H, 1, d, seed=1000 + rank, Lk=hi - lo)
+    if impl == "native":
+        comm = fdist.RcclComm()
+
+        def step():
+            fdist.splitkv_attention_native(q, k, v, comm)
+        kernel = "fa_fwd_kernel (partial) + RCCL send/recv + fa_combine_kernel (C ABI)"
+    else:
+        def step():
+            fdist.splitkv_attention(q, k, v)
+        kernel = "fa_fwd_kernel (partial) + all_to_all + fa_combine_kernel"
+    return step, kernel, flops(B, H, L, d, Lk=hi - lo)
+
+
 def load_traffic(config):
     path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     try:
@@ -187,22 +208,8 @@ def main():
         parallel = f"heads{world}" if world > 1 else "single"
     else:
         # C5: keys of one L=16384 sequence sharded over the ranks; all-to-all combine.
-        lo, hi = fdist.shard_bounds(L, world, rank)
-        q, _, _ = _make_inputs(torch, dev, B, H, L, d, seed=99)  # same Q on every rank
-        _, k, v = _make_inputs(torch, dev, B, H, 1, d, seed=1000 + rank, Lk=hi - lo)
-
-        if args.dist_impl == "native":
-            comm = fdist.RcclComm()
-
-            def step():
-                fdist.splitkv_attention_native(q, k, v, comm)
-            kernel = "fa_fwd_kernel (partial) + RCCL send/recv + fa_combine_kernel (C ABI)"
-        else:
-            def step():
-                fdist.splitkv_attention(q, k, v)
-            kernel = "fa_fwd_kernel (partial) + all_to_all + fa_combine_kernel"
+        step, kernel, work = c5_step(torch, fdist, dev, world, rank, args.dist_impl)  # work: this rank's share
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
-        work = flops(B, H, L, d, Lk=hi - lo)  # this rank's share
         workload = "FA-v2 split-KV forward, keys sharded over ranks"
         parallel = f"kv{world}"
 
@@ -214,6 +221,23 @@ def main():
     ms_per_step = wall / args.steps * 1e3
     total_work = work * world
     value = total_work / (wall / args.steps) / 1e9
+
+    if not args.no_extra and args.mode == "heads":
+        # C5 split-KV over all ranks (north_star: 1/2/4/8-GPU split-KV throughput and achieved
+        # fraction); every rank takes part in the exchange, time = max over ranks
+        st5, _, w5 = c5_step(torch, fdist, dev, world, rank)
+        n5 = 10
+        wall5, ems5 = time_step(torch, st5, n5, 3, barrier)
+        t5 = torch.tensor([wall5, ems5], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t5, op=dist.ReduceOp.MAX)
+        ms5 = float(t5[0]) / n5 * 1e3
+        tf5 = w5 * world / (ms5 * 1e-3) / 1e12
+        extra["c5_splitkv_dist"] = {"ms": round(ms5, 3), "tflops": round(tf5, 1),
+                                    "frac": round(tf5 / (PEAK_BF16_TFLOPS * world), 4), "ranks": world,
+                                    "exchange": "all_to_all_single (RCCL)" if world > 1 else "none"}
+        del st5
+        torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
         # per-variant timings at N=1 (informational; not the headline value)

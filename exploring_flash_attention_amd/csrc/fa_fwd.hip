@@ -85,6 +85,10 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 #ifndef FA_RSRC32
 #define FA_RSRC32 1
 #endif
+// packed fp32 softmax arithmetic for d <= FA_PK_MAXD (0 = off)
+#ifndef FA_PK_MAXD
+#define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
+#endif
 #ifndef FA_QK_LEAD
 #define FA_QK_LEAD 4
 #endif
@@ -289,6 +293,30 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     };
     // P = 2^(S*c - m) in place, and its row sum into l
     auto exp_tile = [&](f32x16 (&s)[RB][NKB]) {
+        if constexpr (D <= FA_PK_MAXD && !FA_MFMA_ROWSUM) {
+            // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU instruction where
+            // the MFMA pipe is mostly idle (small d is VALU-bound)
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const f32x2 c2 = {c, c}, nm2 = {-m[r], -m[r]};
+                f32x2 sum2[2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+                for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                    for (int i = 0; i < 16; i += 2) {
+                        f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
+                        x = __builtin_elementwise_fma(x, c2, nm2);
+                        x[0] = __builtin_amdgcn_exp2f(x[0]);
+                        x[1] = __builtin_amdgcn_exp2f(x[1]);
+                        s[r][b2][i] = x[0];
+                        s[r][b2][i + 1] = x[1];
+                        sum2[(i >> 1) & 1] += x;
+                    }
+                const f32x2 t = sum2[0] + sum2[1];
+                l[r] += t[0] + t[1];
+            }
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             float sum4[4] = {0.f, 0.f, 0.f, 0.f};

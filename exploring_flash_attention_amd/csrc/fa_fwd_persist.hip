@@ -109,7 +109,7 @@ __global__ __launch_bounds__(64 * W, 2) void fa_fwd_persist_kernel(FwdArgs a) {
     };
     int beg_s, end_s;  // static mode: blocks with equal b % 8 take one eighth, round robin
     xcd_range(nitems, (int)(blockIdx.x & 7), beg_s, end_s);
-    const int J = (int)(gridDim.x >> 3), js = (int)(blockIdx.x >> 3);
+    [[maybe_unused]] const int J = (int)(gridDim.x >> 3), js = (int)(blockIdx.x >> 3);
 
     int item;
 #if FA_PQ_STEAL
