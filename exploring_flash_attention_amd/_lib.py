@@ -35,12 +35,15 @@ SIGNATURES = {
     "fa_kernel_geometry": (_I, [_I64, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                 ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "fa_fwd_v1": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
+    "fa_fwd_v1_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, ctypes.c_double, _I, _P]),
     "fa_fwd_v1_w64": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
     "fa_fwd_v1_tiled_d": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P]),
     "fa_fwd_v2_workspace_size": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I,
                                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_I)]),
     "fa_fwd_v2": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
                        _I, _I, _P]),
+    "fa_fwd_v2_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
+                              ctypes.c_double, _I, _I, _P]),
     "fa_fwd_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
     "fa_combine": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
 }

@@ -108,6 +108,16 @@ fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int6
     return a;
 }
 
+// softmax_scale > 0 replaces 1/sqrt(d) (the scaled entry points: a caller that zero-pads the
+// head dim to a kernel's d keeps the scale of the unpadded one)
+int apply_scale(fa::FwdArgs& a, double softmax_scale) {
+    if (!(softmax_scale > 0.0) || !std::isfinite(softmax_scale))
+        return fail(FA_ERR_INVALID_ARG, "softmax_scale must be positive and finite (got %g)", softmax_scale);
+    a.scale_log2_64 = 1.4426950408889634 * softmax_scale;
+    a.scale_log2 = (float)a.scale_log2_64;
+    return FA_OK;
+}
+
 hipError_t launch_final(fa::Elem e, int d, const fa::FwdArgs& a, hipStream_t s) {
     return e == fa::Elem::F64 ? fa::launch_fwd64(d, fa::kFinal, a, s) : fa::launch_fwd(e, e, d, fa::kFinal, a, s);
 }
@@ -202,11 +212,17 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
 
 int fa_fwd_v1(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
               int64_t L, int64_t d, int dtype, void* stream) {
+    return fa_fwd_v1_scaled(q, k, v, o, B, H, L, d, 1.0 / std::sqrt((double)(d > 0 ? d : 1)), dtype, stream);
+}
+
+int fa_fwd_v1_scaled(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
+                     int64_t L, int64_t d, double softmax_scale, int dtype, void* stream) {
     fa::Elem e;
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
+    if (int st = apply_scale(a, softmax_scale)) return st;
     if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1 launch");
     return ok();
@@ -259,6 +275,15 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_
 int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H, int64_t L,
               int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block, void* workspace,
               size_t workspace_bytes, int dtype, int partial_dtype, void* stream) {
+    return fa_fwd_v2_scaled(q, k, v, o, B, H, L, d, d_tile_qk, d_tile_v, kv_tiles_per_block, workspace,
+                            workspace_bytes, 1.0 / std::sqrt((double)(d > 0 ? d : 1)), dtype, partial_dtype,
+                            stream);
+}
+
+int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
+                     int64_t L, int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
+                     void* workspace, size_t workspace_bytes, double softmax_scale, int dtype,
+                     int partial_dtype, void* stream) {
     fa::Elem e, pe;
     size_t need = 0;
     int ns = 0;
@@ -278,6 +303,7 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o, int64_t B, i
 
     const int64_t BH = B * H;
     fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d, e);
+    if (int st = apply_scale(a, softmax_scale)) return st;
     if (ns == 1) {  // one split: nothing to combine
         if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
             return hip_fail(he, "fa_fwd_v2 launch");

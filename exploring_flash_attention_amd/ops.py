@@ -32,7 +32,29 @@ def _default_pdtype(dtype, partial_dtype):
         return partial_dtype
     return torch.float64 if dtype == torch.float64 else torch.float32
 
-SUPPORTED_HEAD_DIMS = (32, 64, 128, 256)
+SUPPORTED_HEAD_DIMS = (32, 64, 128, 256)  # head dims with a kernel
+MAX_HEAD_DIM = 256
+
+
+def kernel_head_dim(d):
+    """Head dim of the kernel that serves head dim d: d itself when a kernel exists,
+    otherwise the next larger one (the operators then zero-pad q, k, v to it and keep the
+    softmax scale 1/sqrt(d); zero columns add nothing to q k^T and come out of P.V as zeros).
+    The reference's Python functions take any d, e.g. d = 16 in its tests' shapes."""
+    d = int(d)
+    if d <= 0 or d > MAX_HEAD_DIM:
+        raise ValueError(f"head dim d={d} unsupported (1 <= d <= {MAX_HEAD_DIM})")
+    return next(D for D in SUPPORTED_HEAD_DIMS if D >= d)
+
+
+def _pad_d(t, D):
+    return t if t.shape[-1] == D else torch.nn.functional.pad(t, (0, D - t.shape[-1])).contiguous()
+
+
+def _unpad_into(o_pad, o, d):
+    if o_pad is not o:
+        o.copy_(o_pad[..., :d])
+    return o
 
 
 def _stream(t):
@@ -85,12 +107,20 @@ def _out(out, q, shape=None, dtype=None):
 
 
 def attention_v1(q, k, v, out=None):
-    """FA-v1 fused forward: O = softmax(q k^T / sqrt(d)) v."""
+    """FA-v1 fused forward: O = softmax(q k^T / sqrt(d)) v.  Any 1 <= d <= 256 (head dims
+    without a kernel are zero-padded to the next one, see kernel_head_dim)."""
     _check_qkv(q, k, v)
     o = _out(out, q)
     B, H, L, d = q.shape
-    check(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
-    return o
+    D = kernel_head_dim(d)
+    if D == d:
+        check(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
+        return o
+    qp, kp, vp = (_pad_d(t, D) for t in (q, k, v))
+    op = torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
+    check(lib().fa_fwd_v1_scaled(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, 1.0 / d ** 0.5,
+                                 _DTYPES[q.dtype], _stream(q)))
+    return _unpad_into(op, o, d)
 
 
 def attention_v1_w64(q, k, v, out=None):
@@ -102,11 +132,26 @@ def attention_v1_w64(q, k, v, out=None):
     return o
 
 
-def attention_tiled_d(q, k, v, d_tile_qk=32, d_tile_v=32, out=None):
-    """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher."""
+def _d_tiles(d, d_tile_qk, d_tile_v):
+    """d tiles default to min(32, d) (the reference's D_TILE = 32 where d allows it)."""
+    return (min(32, d) if d_tile_qk is None else int(d_tile_qk),
+            min(32, d) if d_tile_v is None else int(d_tile_v))
+
+
+def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
+    """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher
+    (0 < d_tile <= d; default min(32, d))."""
     _check_qkv(q, k, v)
-    o = _out(out, q)
     B, H, L, d = q.shape
+    d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
+    if kernel_head_dim(d) != d:
+        # the tile arguments are validated against the true d, as the launcher does
+        # (flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327)
+        for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
+            if not 0 < int(t) <= d:
+                raise _lib.FaArgumentError(1, f"{name}={int(t)} must satisfy 0 < {name} <= d={d}")
+        return attention_v1(q, k, v, out=out)
+    o = _out(out, q)
     check(lib().fa_fwd_v1_tiled_d(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
                                   int(d_tile_v), _DTYPES[q.dtype], _stream(q)))
     return o
@@ -124,12 +169,13 @@ def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes = ctypes.c_size_t()
     ns = ctypes.c_int()
+    d = kernel_head_dim(d)
     check(lib().fa_fwd_v2_workspace_size(B, H, L, d, int(kv_tiles_per_block), _DTYPES[dtype],
                                          _PDTYPES[pd], ctypes.byref(nbytes), ctypes.byref(ns)))
     return nbytes.value, ns.value
 
 
-def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, partial_dtype=None,
+def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, partial_dtype=None,
                  out=None, workspace=None):
     """FA-v2 split-KV forward (partial kernel + combine kernel).
 
@@ -144,6 +190,8 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
     _check_qkv(q, k, v)
     o = _out(out, q)
     B, H, L, d = q.shape
+    D = kernel_head_dim(d)
+    d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
     pd = _default_pdtype(q.dtype, partial_dtype)
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
@@ -151,11 +199,21 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=32, d_tile_v=32, parti
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=q.device)
     elif workspace.numel() * workspace.element_size() < nbytes:
         raise ValueError(f"workspace too small: {nbytes} bytes needed")
-    check(lib().fa_fwd_v2(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
-                          int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace),
-                          workspace.numel() * workspace.element_size(), _DTYPES[q.dtype],
-                          _PDTYPES[pd], _stream(q)))
-    return o
+    wsb = workspace.numel() * workspace.element_size()
+    if D == d:
+        check(lib().fa_fwd_v2(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+                              int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb,
+                              _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
+        return o
+    for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
+        if not 0 < int(t) <= d:
+            raise _lib.FaArgumentError(1, f"{name}={int(t)} must satisfy 0 < {name} <= d={d}")
+    qp, kp, vp = (_pad_d(t, D) for t in (q, k, v))
+    op = torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
+    check(lib().fa_fwd_v2_scaled(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, int(d_tile_qk),
+                                 int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb, 1.0 / d ** 0.5,
+                                 _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
+    return _unpad_into(op, o, d)
 
 
 def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None, lse=None):

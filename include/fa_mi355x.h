@@ -36,7 +36,8 @@
  *     element type is a runtime argument (FA_DTYPE_BF16, FA_DTYPE_FP16 or FA_DTYPE_FP64);
  *   - the reference fixes the head dim at compile time (assert(d == D),
  *     flash_attention_v1/CUDA/flash_attention_v1.h:264); here d is dispatched at run
- *     time to kernels for d in {32, 64, 128, 256}; any other d returns FA_ERR_UNSUPPORTED;
+ *     time to kernels for d in {32, 64, 128, 256}; any other d returns FA_ERR_UNSUPPORTED
+ *     (the *_scaled entry points let a caller zero-pad any d <= 256 to the next one);
  *   - sizes are int64_t and every offset is 64-bit (the reference overflows int32 in
  *     its workspace index at L=4096, flash_attention_v2/CUDA/flash_attention_v2.h:324).
  */
@@ -84,6 +85,16 @@ int fa_fwd_v1(const void* q, const void* k, const void* v, void* o,
               int64_t B, int64_t H, int64_t L, int64_t d,
               int dtype, void* stream);
 
+/* fa_fwd_v1 with an explicit softmax scale: O = softmax(softmax_scale * Q K^T) V.
+ * softmax_scale > 0 and finite (else FA_ERR_INVALID_ARG); fa_fwd_v1 passes 1/sqrt(d).
+ * Lets a caller run a head dim without its own kernel by zero-padding Q, K and V to a
+ * supported d (zero columns add nothing to Q K^T; the padded O columns come out zero)
+ * while keeping the scale of the true head dim -- the reference's Python functions take any
+ * d (e.g. flash_attention_v1/numpy_gpu_like_opt2.py:198 with d = 16); the Python layer
+ * (exploring_flash_attention_amd/ops.py) does exactly this. */
+int fa_fwd_v1_scaled(const void* q, const void* k, const void* v, void* o,
+                     int64_t B, int64_t H, int64_t L, int64_t d, double softmax_scale,
+                     int dtype, void* stream);
 /* FA-v1 d-tiled forward.  d_tile_qk / d_tile_v must satisfy 0 < d_tile <= d
  * (the reference's asserts, flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327),
  * otherwise FA_ERR_INVALID_ARG.  The d-chunking of the arithmetic is set by the MFMA
@@ -128,6 +139,12 @@ int fa_fwd_v2(const void* q, const void* k, const void* v, void* o,
               void* workspace, size_t workspace_bytes,
               int dtype, int partial_dtype, void* stream);
 
+/* fa_fwd_v2 with an explicit softmax scale (as fa_fwd_v1_scaled). */
+int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o,
+                     int64_t B, int64_t H, int64_t L, int64_t d,
+                     int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
+                     void* workspace, size_t workspace_bytes, double softmax_scale,
+                     int dtype, int partial_dtype, void* stream);
 /* Split-KV partial forward over ONE key range (a whole KV shard, e.g. one GPU's
  * slice of the sequence).  q: [B, H, Lq, d]; k, v: [B, H, Lk, d].
  * Writes, for every query row, the normalised partial output and its log-sum-exp

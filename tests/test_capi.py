@@ -77,6 +77,28 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert st == L.FA_ERR_INVALID_ARG and b"aligned" in lib.fa_last_error()
 
 
+def test_scaled_entry_points_validate_scale():
+    lib = L.lib()
+    fake = ctypes.c_void_p(0x10000)
+    for bad in (0.0, -1.0, float("inf"), float("nan")):
+        st = lib.fa_fwd_v1_scaled(fake, fake, fake, fake, 1, 1, 64, 128, bad, L.FA_DTYPE_BF16, NULL)
+        assert st == L.FA_ERR_INVALID_ARG and b"softmax_scale" in lib.fa_last_error()
+    st = lib.fa_fwd_v1_scaled(fake, fake, fake, fake, 1, 1, 64, 48, 0.1, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED  # the scaled entry still needs a kernel head dim
+    st = lib.fa_fwd_v2_scaled(fake, fake, fake, fake, 1, 1, 64, 128, 32, 32, 1, NULL, 0, -2.0,
+                              L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
+    assert st != L.FA_OK
+
+
+def test_kernel_head_dim_padding_map():
+    from exploring_flash_attention_amd import ops
+    assert [ops.kernel_head_dim(d) for d in (1, 16, 32, 33, 48, 64, 80, 96, 128, 129, 200, 256)] == \
+        [32, 32, 32, 64, 64, 64, 128, 128, 128, 256, 256, 256]
+    for bad in (0, -4, 257, 512):
+        with pytest.raises(ValueError):
+            ops.kernel_head_dim(bad)
+
+
 def test_workspace_size_and_v2_checks():
     lib = L.lib()
     nbytes, ns = ctypes.c_size_t(), ctypes.c_int()

@@ -176,6 +176,41 @@ def test_matrix(gpu, variant, dtype, d):
         _gate(out, _ref(q, k, v), dtype)
 
 
+@pytest.mark.parametrize("d", [8, 16, 48, 80, 96, 160, 200])
+def test_head_dims_without_a_kernel(gpu, d):
+    """Any 1 <= d <= 256: zero-padded to the next kernel head dim with the scale 1/sqrt(d)
+    (fa_fwd_v1_scaled / fa_fwd_v2_scaled); every variant, bf16 and fp64 (bit-tight)."""
+    for i, (B, H, L) in enumerate([(1, 2, 65), (2, 1, 200)]):
+        q, k, v = _inputs(B, H, L, d, torch.bfloat16, seed=10 + i)
+        ref = _ref(q, k, v)
+        from exploring_flash_attention_amd import ops
+        variants = dict(_variants())
+        variants["tiled_d"] = lambda a, b, c: ops.attention_tiled_d(a, b, c, min(16, d), min(32, d))
+        for name, fn in variants.items():
+            out = fn(q.to(gpu), k.to(gpu), v.to(gpu))
+            torch.cuda.synchronize()
+            assert out.shape == q.shape and out.dtype == torch.bfloat16 and out.is_contiguous(), name
+            _gate(out, ref, torch.bfloat16)
+        q64, k64, v64 = (x.double().to(gpu) for x in (q, k, v))
+        with pytest.raises(ValueError):  # tiles are checked against the true d
+            ops.attention_tiled_d(q.to(gpu), k.to(gpu), v.to(gpu), d + 1, 1)
+        for fn in (ops.attention_v1, lambda a, b, c: ops.attention_v2(a, b, c, 1)):
+            o64 = fn(q64, k64, v64).cpu().numpy()
+            assert np.abs(o64 - ref).max() <= 1e-12
+
+
+def test_golden_flat_surface_d16(gpu):
+    """The reference's own d = 16 case (numpy_gpu_like_opt2.py surface, L = 40): fp64 in,
+    fp64 kernel on the zero-padded d = 32, 1e-12 against the reference's output."""
+    from exploring_flash_attention_amd import v1
+    g = golden("g2_v1_opt2_L40_d16.npz")
+    L, d = g["Q"].shape
+    O = np.zeros(L * d)
+    assert v1.flash_attention_tiled(g["Q"].ravel(), g["K"].ravel(), g["V"].ravel(), O, L, d, 8, 8) is None
+    check_accuracy(O.reshape(L, d), g["O"])
+    assert np.abs(O.reshape(L, d) - g["O"]).max() <= 1e-12
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
 def test_uniform_inputs(gpu, dtype):
     from exploring_flash_attention_amd import ops
