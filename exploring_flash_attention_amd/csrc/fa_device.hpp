@@ -51,9 +51,14 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// max without fmaxf's IEEE quieting: llvm.maximum lowers to v_maximum3_f32 on gfx950 and
+// needs no canonicalising v_max x,x in front of every MFMA result it reads (NaN propagates
+// instead of being dropped -- scores are finite or -inf here)
+__device__ __forceinline__ float fmax_nc(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
 __device__ __forceinline__ float pair_max(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    return fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ __forceinline__ float pair_sum(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);

@@ -85,6 +85,10 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 #ifndef FA_RSRC32
 #define FA_RSRC32 1
 #endif
+// row max on v_maximum3_f32 (no canonicalising v_max x,x per MFMA result)
+#ifndef FA_MAXNC
+#define FA_MAXNC 1
+#endif
 // packed fp32 softmax arithmetic for d <= FA_PK_MAXD (0 = off)
 #ifndef FA_PK_MAXD
 #define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
@@ -361,8 +365,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
-                    if (b2 > 0 || i >= 4) mx4[i & 3] = fmaxf(mx4[i & 3], s[r][b2][i]);
-            mx[r] = pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
+                    if (b2 > 0 || i >= 4) mx4[i & 3] = FA_MAXNC ? fmax_nc(mx4[i & 3], s[r][b2][i]) : fmaxf(mx4[i & 3], s[r][b2][i]);
+            mx[r] = FA_MAXNC ? pair_max(fmax_nc(fmax_nc(mx4[0], mx4[1]), fmax_nc(mx4[2], mx4[3]))) * c
+                             : pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
         }
     };
     // V^T fragments of (32-key block b2, 32-column block db): 4 transposed reads of 4
