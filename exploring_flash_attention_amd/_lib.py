@@ -36,6 +36,7 @@ SIGNATURES = {
                                 ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "fa_fwd_v1": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
     "fa_fwd_v1_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, ctypes.c_double, _I, _P]),
+    "fa_fwd_v1_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, ctypes.c_double, _I, _P]),
     "fa_fwd_v1_w64": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
     "fa_fwd_v1_tiled_d": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P]),
     "fa_fwd_v2_workspace_size": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I,
@@ -44,6 +45,8 @@ SIGNATURES = {
                        _I, _I, _P]),
     "fa_fwd_v2_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
                               ctypes.c_double, _I, _I, _P]),
+    "fa_fwd_v2_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
+                          _P, _P, _P, ctypes.c_double, _I, _I, _P]),
     "fa_fwd_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
     "fa_combine": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
 }

@@ -108,6 +108,38 @@ fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int6
     return a;
 }
 
+// Strided views ([B, H, L, d] with element strides {batch, head, row}, d contiguous; NULL =
+// contiguous).  Every row start must stay 16-byte aligned (the kernel loads 16 B per lane)
+// and one head's rows must span < 2 GiB (32-bit buffer offsets).
+int apply_strides(fa::FwdArgs& a, fa::Elem e, int64_t B, int64_t H, int64_t L, int64_t d,
+                  const int64_t* qs, const int64_t* kvs, const int64_t* os) {
+    a.H = H;
+    if (!qs && !kvs && !os) return FA_OK;
+    if (e == fa::Elem::F64) return fail(FA_ERR_UNSUPPORTED, "strided tensors: bf16 / fp16 only");
+    const int64_t contig[3] = {H * L * d, L * d, d};
+    const int64_t* st[3] = {qs ? qs : contig, kvs ? kvs : contig, os ? os : contig};
+    const char* names[3] = {"q", "k/v", "o"};
+    for (int t = 0; t < 3; ++t) {
+        for (int i = 0; i < 3; ++i) {
+            if (st[t][i] <= 0 || (st[t][i] * 2) % 16)
+                return fail(FA_ERR_INVALID_ARG, "%s stride[%d]=%lld must be positive and a multiple of 8 elements",
+                            names[t], i, (long long)st[t][i]);
+        }
+        if (st[t][2] < d)
+            return fail(FA_ERR_INVALID_ARG, "%s row stride %lld < d=%lld", names[t], (long long)st[t][2], (long long)d);
+        if ((L - 1) * st[t][2] * 2 + d * 2 > 0x7fffffffLL)
+            return fail(FA_ERR_UNSUPPORTED, "%s: one head's rows span more than 2 GiB", names[t]);
+        (void)B;
+    }
+    a.strided = 1;
+    for (int i = 0; i < 3; ++i) {
+        a.q_stride[i] = st[0][i];
+        a.k_stride[i] = st[1][i];
+        a.o_stride[i] = st[2][i];
+    }
+    return FA_OK;
+}
+
 // softmax_scale > 0 replaces 1/sqrt(d) (the scaled entry points: a caller that zero-pads the
 // head dim to a kernel's d keeps the scale of the unpadded one)
 int apply_scale(fa::FwdArgs& a, double softmax_scale) {
@@ -217,12 +249,19 @@ int fa_fwd_v1(const void* q, const void* k, const void* v, void* o, int64_t B, i
 
 int fa_fwd_v1_scaled(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
                      int64_t L, int64_t d, double softmax_scale, int dtype, void* stream) {
+    return fa_fwd_v1_ex(q, k, v, o, B, H, L, d, nullptr, nullptr, nullptr, softmax_scale, dtype, stream);
+}
+
+int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H, int64_t L,
+                 int64_t d, const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
+                 double softmax_scale, int dtype, void* stream) {
     fa::Elem e;
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
+    if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
     if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1 launch");
     return ok();
@@ -284,6 +323,14 @@ int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o, int64
                      int64_t L, int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
                      void* workspace, size_t workspace_bytes, double softmax_scale, int dtype,
                      int partial_dtype, void* stream) {
+    return fa_fwd_v2_ex(q, k, v, o, B, H, L, d, d_tile_qk, d_tile_v, kv_tiles_per_block, workspace,
+                        workspace_bytes, nullptr, nullptr, nullptr, softmax_scale, dtype, partial_dtype, stream);
+}
+
+int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H, int64_t L,
+                 int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block, void* workspace,
+                 size_t workspace_bytes, const int64_t* q_strides, const int64_t* kv_strides,
+                 const int64_t* o_strides, double softmax_scale, int dtype, int partial_dtype, void* stream) {
     fa::Elem e, pe;
     size_t need = 0;
     int ns = 0;
@@ -304,6 +351,7 @@ int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o, int64
     const int64_t BH = B * H;
     fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
+    if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
     if (ns == 1) {  // one split: nothing to combine
         if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
             return hip_fail(he, "fa_fwd_v2 launch");

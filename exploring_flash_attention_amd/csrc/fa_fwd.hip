@@ -1,762 +1,10 @@
-// fa_fwd.hip -- flash-attention forward for MI355X (gfx950 / CDNA4).
-//
-// One kernel template serves the three reference kernel families:
-//   final mode   (MODE=kFinal): FA-v1 fused / d-tiled forward
-//                 <- flash_attention_kernel    flash_attention_v1/CUDA/flash_attention_v1.h:161
-//                 <- flash_attention_kernel_opt1 flash_attention_v1/CUDA/flash_attention_v1_opt1.h:264
-//                 <- flash_attention_kernel (tiled-d) flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:230
-//   partial mode (MODE=kPartial): FA-v2 split-KV partial kernel (+ fa_combine.hip)
-//                 <- partial_attention_kernel  flash_attention_v2/CUDA/flash_attention_v2.h:243
-//   fused split  (MODE=kFused): the same partials, combined by the last workgroup of each
-//                 query tile to finish (the reduction_kernel's maths,
-//                 flash_attention_v2/CUDA/flash_attention_v2.h:356, without its HBM pass)
-//
-// Online-softmax recurrence per KV tile (flash_attention_v1/numpy_gpu_like_opt2.py:135-195):
-//   S = Q K^T * scale; m_new = max(m, rowmax S); alpha = e^(m - m_new);
-//   P = e^(S - m_new); l = l*alpha + rowsum P; O = O*alpha + P V;  finally O / l.
-// Here the exponentials are base 2 with log2(e)/sqrt(d) folded into one FMA.
-//
-// Mapping to CDNA4 (see DESIGN.md for the derivation):
-//   * workgroup = 4 waves x 32 query rows = 128 rows of one (b,h); KV tiles of 64 keys.
-//   * S^T = K . Q^T on v_mfma_f32_32x32x16 (A = K rows from LDS via ds_read_b128,
-//     B = Q^T fragments held in VGPRs for the whole KV loop): the accumulator puts one
-//     query row per lane (lanes l and l+32 share a row), so row max / row sum are
-//     in-lane plus one v_permlane32_swap.
-//   * O^T = V^T . P^T: the S accumulator, exponentiated and packed to 16-bit, is already
-//     the B operand (no LDS round trip); V^T fragments come from ds_read_b64_tr_b16
-//     transposed LDS reads.  O_acc stays in VGPRs/AGPRs for the whole KV loop.
-//   * K and V tiles go HBM -> LDS by LDS-DMA (buffer_load ... lds) into a double-buffered,
-//     XOR-swizzled LDS image that is bank-conflict-free for both the row reads and the
-//     transposed reads.
-//   * blockIdx is remapped so that all query tiles of one (b,h) land on one XCD and
-//     share that head's K/V in the XCD's L2.
-#include "fa_device.hpp"
-
-// Build knobs for A/B experiments (scripts/build_variants.sh, scripts/ab.py); the
-// defaults are the measured-best settings.  FA_ABL_* are ablations (wrong results,
-// timing only) used to attribute time to the kernel's phases.
-#ifndef FA_QK_SCHED
-#define FA_QK_SCHED 0
-#endif
-#ifndef FA_WIDE_STORE
-#define FA_WIDE_STORE 1
-#endif
-// FA_MFMA_ROWSUM: the softmax denominator as one more MFMA column block (ones . P^T)
-// instead of 32 VALU adds per tile: sums the same 16-bit-rounded P the numerator uses.
-// Default off: -4 % at d=128, within noise at d=32 (A/B).
-#ifndef FA_MFMA_ROWSUM_MAXD
-#define FA_MFMA_ROWSUM_MAXD 0
-#endif
-#ifndef FA_DMA_LATE
-#define FA_DMA_LATE 1
-#endif
-#ifndef FA_PRIO
-#define FA_PRIO 0
-#endif
-#ifndef FA_ROWMAX_FENCE
-#define FA_ROWMAX_FENCE 1
-#endif
-#ifndef FA_ABL_NODMAWAIT
-#define FA_ABL_NODMAWAIT 0
-#endif
-#ifndef FA_ABL_NOEXP
-#define FA_ABL_NOEXP 0
-#endif
-#ifndef FA_ABL_NODMA
-#define FA_ABL_NODMA 0
-#endif
-#ifndef FA_ABL_NOPV
-#define FA_ABL_NOPV 0
-#endif
-#ifndef FA_ABL_NOQK
-#define FA_ABL_NOQK 0
-#endif
-// readfirstlane wave id (the DMA's M0 values become SGPR arithmetic): a bitmask over
-// d = 32/64/128/256 (bits 0..3).  A/B with the no-tail step: d=32 +3 %, d=64 0, d=128 -1.7 %.
-#ifndef FA_UNIFORM_WID
-#define FA_UNIFORM_WID 1
-#endif
-// the no-tail specialisation (TAIL = false) per d, same bitmask: d=32 +1.6 %, d=128 +0.5 %,
-// d=64 -7 % (hipcc's schedule of the single-block step is worse there)
-#ifndef FA_NOTAIL_MASK
-#define FA_NOTAIL_MASK 0xD
-#endif
-constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
-#ifndef FA_RSRC32
-#define FA_RSRC32 1
-#endif
-// row max on v_maximum3_f32 (no canonicalising v_max x,x per MFMA result)
-#ifndef FA_MAXNC
-#define FA_MAXNC 1
-#endif
-// packed fp32 softmax arithmetic for d <= FA_PK_MAXD (0 = off)
-#ifndef FA_PK_MAXD
-#define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
-#endif
-#ifndef FA_QK_LEAD
-#define FA_QK_LEAD 4
-#endif
-
-// FA_STAMPS (diagnostic builds only): wave 0 of every workgroup writes s_memtime stamps at
-// the phase boundaries into g_fa_stamps (never into an output), read back through
-// fa_debug_stamps() by scripts/stamps.py.  Slots per workgroup: 0 entry, 1 Q/K0/V0/K1
-// landed, 2 loop start, 3 loop end, 4 stores issued, 5 stores retired, 6 hw_id, 7 xcc_id,
-// 8 / 9 s_memrealtime (100 MHz, one time base for all CUs) at entry / after the stores retired.
-#ifndef FA_STAMPS
-#define FA_STAMPS 0
-#endif
-#if FA_STAMPS
-#define FA_MAX_STAMP_WG 65536
-__device__ unsigned long long g_fa_stamps[FA_MAX_STAMP_WG * 16];
-#define FA_STAMP_V(i, v)                                                                       \
-    do {                                                                                       \
-        if (tid == 0 && blockIdx.x < FA_MAX_STAMP_WG)                                          \
-            __hip_atomic_store(&g_fa_stamps[blockIdx.x * 16 + (i)], (unsigned long long)(v),     \
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     \
-    } while (0)
-#define FA_STAMP(i) FA_STAMP_V(i, __builtin_amdgcn_s_memtime())
-extern "C" int fa_debug_stamps(void* dst, size_t bytes) {
-    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fa_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-#else
-#define FA_STAMP_V(i, v) \
-    do {                 \
-    } while (0)
-#define FA_STAMP(i) FA_STAMP_V(i, 0)
-#endif
+// fa_fwd.hip -- launchers of the forward kernel (fa_fwd_kernel.hpp) on contiguous
+// [B, H, L, d] tensors; strided tensors go to fa_fwd_strided.hip (a separate translation
+// unit, so the two instantiation sets compile in parallel).
+#define FA_FWD_MAIN_TU
+#include "fa_fwd_kernel.hpp"
 
 namespace fa {
-
-// TAIL: Lk is not a multiple of the KV tile, so the last tile of a split is partial (key
-// mask, clamped DMA descriptor).  Without it the steady-state step has no mask branch, which
-// would otherwise split the step into basic blocks and push the row sums out of the MFMA block.
-template <typename T, typename PT, int D, int MODE, bool TAIL>
-__global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(FwdArgs a) {
-    using M = Mma<T>;
-    using v8 = typename M::v8;
-    constexpr int RB = kRB;                   // 32-row query blocks per wave
-    constexpr int ROWB = D * 2;               // bytes per LDS row
-    constexpr int kBK = bk_for(D);            // keys per KV tile
-    constexpr int TILEB = kBK * ROWB;         // bytes of one K (or V) tile
-    constexpr int NKS = D / 16;               // MFMA k-steps of Q K^T
-    constexpr int NDB = D / 32;               // 32-column blocks of O
-    constexpr int NKB = kBK / 32;             // 32-key blocks per KV tile
-    // Deferred rescale (defer-max): the reference max m of a row is only moved when some
-    // row of the wave's block sees a tile max above m + kThr (log2 units); P is then
-    // bounded by 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows
-    // (the dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
-    constexpr float kThr = 4.f;
-    constexpr bool FA_MFMA_ROWSUM = D <= FA_MFMA_ROWSUM_MAXD;
-
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    // LDS: K ring (2 slots) then V ring (2 slots), one [kBK][D] tile image per slot.
-    char* const kring = smem;
-    char* const vring = smem + 2 * TILEB;
-
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const int qt = w % a.nqt;
-    const int rest = w / a.nqt;
-    const int split = rest % a.nsplit;
-    const int64_t bh = rest / a.nsplit;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    // wave-uniform and PROVABLY so (an SGPR): the LDS-DMA destinations (M0) derived from it
-    // then need no v_readfirstlane per DMA, and no VGPRs hold per-piece LDS addresses
-    const int wid = (FA_UNIFORM_WID & d_bit(D)) ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
-    const int l32 = lane & 31;
-    const int hf = lane >> 5;
-
-    FA_STAMP_V(8, __builtin_amdgcn_s_memrealtime());
-    FA_STAMP(0);
-    FA_STAMP_V(6, __builtin_amdgcn_s_getreg(4 | (31 << 11)));   // HW_REG_HW_ID, 32 bits
-    FA_STAMP_V(7, __builtin_amdgcn_s_getreg(20 | (31 << 11)));  // HW_REG_XCC_ID
-    const int64_t kv_begin = (int64_t)split * a.kv_per_split;
-    const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
-    const int nkv = (int)(kv_end - kv_begin);
-    const int ntiles = (nkv + kBK - 1) / kBK;
-
-    // Buffer descriptors: K/V cover exactly this split's keys, so the DMA of the last
-    // (partial) tile reads zeros past kv_end with no clamping code.
-    const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D;
-    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, a.Lq * ROWB);
-    // K/V of this split; a tile's descriptor (made per DMA, scalar arithmetic only) starts
-    // at the tile and ends at the split's last key, so the hardware range check -- which
-    // does not rely on soffset -- zero-fills the rows of a partial last tile.
-    const unsigned short* const kbase = (const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D;
-    const unsigned short* const vbase = (const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D;
-
-    // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7] of each of its
-    // RB row blocks.  Rows past Lq read zeros and are never stored.
-    const int64_t q_row0 = (int64_t)qt * kBQ + wid * kRowsPerWave + l32;
-    v8 qf[RB][NKS];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-        const int qoff = (int)((q_row0 + 32 * r) * ROWB) + hf * 16;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
-            qf[r][ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, qoff + ks * 32, 0, 0));
-    }
-
-    // K/V tiles go HBM -> LDS by LDS-DMA (buffer_load ... lds): no staging VGPRs, no
-    // ds_write pass.  One wave instruction writes 1 KiB of LDS lane-linearly (M0 base +
-    // 16*lane), so the swizzled image is produced by giving each lane the SOURCE chunk
-    // that lds_off() places at its destination byte.
-    constexpr int NDMA = TILEB / 1024;                      // 1 KiB pieces per tile
-    constexpr int DPW = NDMA >= kWaves ? NDMA / kWaves : 1;  // pieces per (active) wave
-    static_assert(NDMA % kWaves == 0 || kWaves % NDMA == 0, "tile pieces must split over waves");
-    const bool dma_wave = wid * DPW < NDMA;                  // waves past the last piece idle
-    int dma_src[DPW];
-#pragma unroll
-    for (int i = 0; i < DPW; ++i) {
-        const int b = (wid * DPW + i) * 1024 + lane * 16;  // destination byte in the tile image
-        const int rg = b / (8 * ROWB), rem = b % (8 * ROWB);
-        const int row = 8 * rg + (rem % 512) / 64;
-        const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
-        dma_src[i] = row * ROWB + ch * 16;
-    }
-    auto dma_tile = [&](const unsigned short* base, char* slot, int t) {
-        // descriptor over exactly the tile's valid keys (32-bit scalar arithmetic)
-        // (readfirstlane: hipcc evaluates the clamp with v_med3, and a descriptor word it
-        // cannot prove uniform turns every buffer op into a waterfall loop -- T20)
-#if FA_RSRC32
-        const int rem = nkv - t * kBK;
-        const int valid = TAIL ? __builtin_amdgcn_readfirstlane(rem < kBK ? (rem > 0 ? rem : 0) : kBK)
-                               : (t < ntiles ? kBK : 0);
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc32((const char*)base + (int64_t)t * TILEB, valid * ROWB);
-#else
-        const int64_t off = (int64_t)t * TILEB;
-        const int64_t kv_bytes = (int64_t)nkv * ROWB;
-        const __amdgpu_buffer_rsrc_t rs =
-            make_rsrc((const char*)base + off, kv_bytes > off ? kv_bytes - off : 0);
-#endif
-        if (NDMA >= kWaves || dma_wave) {
-#pragma unroll
-            for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], 0);
-        }
-    };
-
-    // transposed-read geometry (constant per lane)
-    const int grp = lane >> 4, gi = lane & 15;
-    const int tr_row = 4 * (grp >> 1) + (gi >> 2);
-    const int tr_col = 16 * (grp & 1) + 4 * (gi & 3);
-
-    f32x16 o[RB][NDB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) o[r][db] = f32x16{};
-    float m[RB], l[RB];  // reference max (log2 units) and this lane's half of the row sum
-    f32x16 lsum[RB];     // FA_MFMA_ROWSUM: every register = the row sum of the lane's query
-#pragma unroll
-    for (int r = 0; r < RB; ++r) lsum[r] = f32x16{};
-    v8 ones;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ones[j] = static_cast<T>(1.0f);
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-        m[r] = -INFINITY;
-        l[r] = 0.f;
-    }
-    const float c = a.scale_log2;
-
-    // S^T[key][q] = K . Q^T for one tile (two 32-key blocks), every K fragment feeding the
-    // RB row blocks.  Fragments are read in groups of two k-steps, one group ahead.
-    auto qk = [&](const char* kb, f32x16 (&s)[RB][NKB]) {
-        constexpr int G = 2;  // k-steps per read group
-        v8 kf[2][NKB][G];     // [buffer][b2][k-step in group]
-        auto rd = [&](int g, v8 (&dst)[NKB][G]) {
-#pragma unroll
-            for (int j = 0; j < G; ++j)
-#pragma unroll
-                for (int b2 = 0; b2 < NKB; ++b2)
-                    dst[b2][j] = *(const v8*)(kb + lds_off<D>(b2 * 32 + l32, 2 * (g * G + j) + hf));
-        };
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2) s[r][b2] = f32x16{};
-        rd(0, kf[0]);
-#pragma unroll
-        for (int g = 0; g < NKS / G; ++g) {
-            if (g + 1 < NKS / G) rd(g + 1, kf[(g + 1) & 1]);
-#pragma unroll
-            for (int j = 0; j < G; ++j)
-#pragma unroll
-                for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                    for (int r = 0; r < RB; ++r) {
-#if FA_ABL_NOQK
-                        asm volatile("" ::"v"(kf[g & 1][b2][j]));
-                        s[r][b2][j] += (float)qf[r][g * G + j][0];
-#else
-                        s[r][b2] = M::mma(kf[g & 1][b2][j], qf[r][g * G + j], s[r][b2]);
-#endif
-                    }
-        }
-    };
-    // P = 2^(S*c - m) in place, and its row sum into l
-    auto exp_tile = [&](f32x16 (&s)[RB][NKB]) {
-        if constexpr (D <= FA_PK_MAXD && !FA_MFMA_ROWSUM) {
-            // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU instruction where
-            // the MFMA pipe is mostly idle (small d is VALU-bound)
-#pragma unroll
-            for (int r = 0; r < RB; ++r) {
-                const f32x2 c2 = {c, c}, nm2 = {-m[r], -m[r]};
-                f32x2 sum2[2] = {{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-                for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                    for (int i = 0; i < 16; i += 2) {
-                        f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
-                        x = __builtin_elementwise_fma(x, c2, nm2);
-                        x[0] = __builtin_amdgcn_exp2f(x[0]);
-                        x[1] = __builtin_amdgcn_exp2f(x[1]);
-                        s[r][b2][i] = x[0];
-                        s[r][b2][i + 1] = x[1];
-                        sum2[(i >> 1) & 1] += x;
-                    }
-                const f32x2 t = sum2[0] + sum2[1];
-                l[r] += t[0] + t[1];
-            }
-            return;
-        }
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            float sum4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-#if FA_ABL_NOEXP
-                    s[r][b2][i] = __builtin_fmaf(s[r][b2][i], c, -m[r]);
-#else
-                    s[r][b2][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][b2][i], c, -m[r]));
-#endif
-                    if (!FA_MFMA_ROWSUM) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
-                }
-            if (!FA_MFMA_ROWSUM) l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
-        }
-    };
-    // keys past the end of the split (only in the last, partial tile) -> -inf
-    auto mask = [&](int t, f32x16 (&s)[RB][NKB]) {
-        const int valid = nkv - t * kBK;
-        if (valid < kBK) {
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int key = b2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-                    if (key >= valid) {
-#pragma unroll
-                        for (int r = 0; r < RB; ++r) s[r][b2][i] = -INFINITY;
-                    }
-                }
-        }
-    };
-    // row max of a (masked) tile, both lane halves, in log2 units
-    auto rowmax = [&](const f32x16 (&s)[RB][NKB], float (&mx)[RB]) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            float mx4[4];  // 4 independent chains over the tile's 16*NKB values
-#pragma unroll
-            for (int j = 0; j < 4; ++j) mx4[j] = s[r][0][j];
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    if (b2 > 0 || i >= 4) mx4[i & 3] = FA_MAXNC ? fmax_nc(mx4[i & 3], s[r][b2][i]) : fmaxf(mx4[i & 3], s[r][b2][i]);
-            mx[r] = FA_MAXNC ? pair_max(fmax_nc(fmax_nc(mx4[0], mx4[1]), fmax_nc(mx4[2], mx4[3]))) * c
-                             : pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
-        }
-    };
-    // V^T fragments of (32-key block b2, 32-column block db): 4 transposed reads of 4
-    // keys; element j of the A operand is key 16*ss + 8*(j>>2) + 4*hf + (j&3), the same
-    // key as element j of the P^T B operand.  Inline asm: hipcc cannot prove the builtin
-    // form disjoint from the in-flight LDS-DMA and would drain it (vmcnt(0)) before every
-    // read; vwait() waits for them and names every destination.  Every read is one of two
-    // per-lane base addresses (key rows +0 / +8, whose swizzles differ) plus an immediate:
-    // lds_off(row + 32*b2 + 16*ss, ch + 4*db) = lds_off(row, ch) + (4*b2 + 2*ss)*8*ROWB + 512*db.
-    // (the V ring's base is in the address registers, keeping every immediate < 64 KiB)
-    const unsigned vbase0 =
-        (unsigned)(size_t)vring + lds_off<D>(tr_row, tr_col >> 3) + (tr_col & 7) * 2;
-    const unsigned vbase1 =
-        (unsigned)(size_t)vring + lds_off<D>(tr_row + 8, tr_col >> 3) + (tr_col & 7) * 2 - 8 * ROWB;
-    auto read_v = [](auto slot_c, auto i_c, u32x2 (&vf)[2][2], unsigned vbase0, unsigned vbase1) {
-        constexpr int SLOT = decltype(slot_c)::value, I = decltype(i_c)::value;
-        constexpr int B2 = I / NDB, DB = I % NDB;
-        constexpr int OFF = SLOT * TILEB + 4 * B2 * 8 * ROWB + 512 * DB;
-        constexpr int SSO = 2 * 8 * ROWB;  // +16 key rows (k-step ss = 1)
-        static_assert(OFF + SSO + 8 * ROWB < 65536, "ds offset field is 16 bits");
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[0][0]) : "v"(vbase0), "i"(OFF) : "memory");
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[0][1]) : "v"(vbase1), "i"(OFF + 8 * ROWB) : "memory");
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[1][0]) : "v"(vbase0), "i"(OFF + SSO) : "memory");
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[1][1]) : "v"(vbase1), "i"(OFF + SSO + 8 * ROWB) : "memory");
-    };
-    auto vwait = [&](u32x2 (&vf)[2][2]) {
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(vf[0][0]), "+v"(vf[0][1]), "+v"(vf[1][0]), "+v"(vf[1][1]));
-    };
-
-    // One pipeline step for tile t, whose raw (masked) scores are in sc and row max in mx:
-    //   DMA K(t+2), V(t+1) into the ring slots freed by the previous step's barrier;
-    //   rescale decision; QK^T(t+1) -> sn beside exp / sum of sc; pack P;
-    //   P.V(t), then mask + row max of sn;  barrier (which also drains the DMA).
-    // P = t & 1 is a compile-time constant (the loop runs steps in pairs).
-    auto step = [&](auto par_c, auto flags_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
-                    float (&mx)[RB]) {
-        constexpr int P = decltype(par_c)::value;
-        // Compile-time step flags, so that QK^T(t+1), the exponentials, the packing, P.V(t)
-        // and the row max of tile t+1 form ONE basic block the scheduler can interleave
-        // (runtime `if`s split it: hipcc hoisted the shared exp code into a join block,
-        // away from the MFMAs).
-        //   MORE      tile t+1 exists
-        //   MASKNEXT  tile t+1 may be the partial last tile (needs the key mask)
-        //   DMAK      tile t+2 exists (its K is prefetched now)
-        constexpr int F = decltype(flags_c)::value;
-        constexpr bool MORE = F & 1, MASKNEXT = TAIL && (F & 2), DMAK = F & 4;
-#if !FA_DMA_LATE
-        if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(kbase, kring + P * TILEB, t + 2);
-        if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
-#endif
-
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            if (__builtin_amdgcn_ballot_w64(mx[r] > m[r] + kThr)) {
-                const float m_new = fmaxf(m[r], mx[r]);
-                const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
-                m[r] = m_new;
-                l[r] *= alpha;
-                if (FA_MFMA_ROWSUM) lsum[r] *= alpha;
-#pragma unroll
-                for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
-            }
-        }
-
-#if FA_DMA_LATE
-        // DMA issued in the MFMA block (the scheduler spreads the pieces among the MFMAs);
-        // tile counts are checked against the compile-time MORE where possible
-        if constexpr (!FA_ABL_NODMA && DMAK) dma_tile(kbase, kring + P * TILEB, t + 2);
-        if constexpr (!FA_ABL_NODMA && MORE) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
-#endif
-#if FA_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
-        if constexpr (MORE) qk(kring + (1 - P) * TILEB, sn);
-        exp_tile(sc);
-        v8 pb[RB][NKB][2];
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    u32x4 u;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        u[j] = pack2<T>(sc[r][b2][8 * ss + 2 * j], sc[r][b2][8 * ss + 2 * j + 1]);
-                    pb[r][b2][ss] = __builtin_bit_cast(v8, u);
-                }
-
-        // O^T[dv][q] += V^T[dv][key] . P^T[key][q]; reads of the next (b2, db) block
-        // overlap this block's MFMAs.
-        u32x2 vcur[2][2], vnext[2][2];
-        read_v(par_c, std::integral_constant<int, 0>{}, vcur, vbase0, vbase1);
-        vwait(vcur);
-        static_for<NKB * NDB>([&](auto i_c) {
-            constexpr int I = decltype(i_c)::value;
-            constexpr int B2 = I / NDB, DB = I % NDB;
-            if constexpr (I + 1 < NKB * NDB)
-                read_v(par_c, std::integral_constant<int, I + 1>{}, vnext, vbase0, vbase1);
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                const u32x4 vv = {vcur[ss][0][0], vcur[ss][0][1], vcur[ss][1][0], vcur[ss][1][1]};
-#pragma unroll
-                for (int r = 0; r < RB; ++r) {
-#if FA_ABL_NOPV
-                    asm volatile("" ::"v"(vv), "v"(pb[r][B2][ss]));
-#else
-                    o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
-#endif
-                    if (FA_MFMA_ROWSUM && DB == 0) lsum[r] = M::mma(ones, pb[r][B2][ss], lsum[r]);
-                }
-            }
-            if constexpr (I + 1 < NKB * NDB) {
-                vwait(vnext);
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    vcur[ss][0] = vnext[ss][0];
-                    vcur[ss][1] = vnext[ss][1];
-                }
-            }
-        });
-        if constexpr (MORE) {
-#if FA_ROWMAX_FENCE
-            __builtin_amdgcn_sched_barrier(0);
-#endif
-            if constexpr (MASKNEXT) mask(t + 1, sn);
-            rowmax(sn, mx);
-        }
-#if FA_ABL_NODMAWAIT
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#else
-#if FA_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-        __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
-#endif
-    };
-
-    // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
-    dma_tile(kbase, kring, 0);
-    dma_tile(vbase, vring, 0);
-    if (ntiles > 1) dma_tile(kbase, kring + TILEB, 1);
-    // Q's loads must retire here: otherwise hipcc's waitcnt pass carries them into the loop
-    // header and, merging with the back edge, waits vmcnt(N) in front of every MFMA.
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[r][ks]));
-    __syncthreads();
-    FA_STAMP(1);
-    f32x16 sa[RB][NKB], sb[RB][NKB];
-    float mx[RB];
-    qk(kring, sa);
-    if constexpr (TAIL) mask(0, sa);
-    rowmax(sa, mx);
-    __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
-    FA_STAMP(2);
-
-    {
-        using C0 = std::integral_constant<int, 0>;
-        using C1 = std::integral_constant<int, 1>;
-        // flags: 1 = MORE, 2 = MASKNEXT, 4 = DMAK (see step)
-        using STEADY = std::integral_constant<int, 1 | 4>;     // t+1, t+2 exist, t+1 not last
-        using NEXTLAST = std::integral_constant<int, 1 | 2>;   // t+1 is the last tile
-        using NEXTLASTK = std::integral_constant<int, 1 | 2 | 4>;
-        using LAST = std::integral_constant<int, 0>;
-        int t = 0;
-        for (; t + 2 < ntiles; t += 2) {
-            // step t: tile t+1 is never the last one here.  Step t+1 may prefetch K(t+3)
-            // past the end: the buffer range check turns it into zeros nobody reads, which
-            // keeps the step branch-free.
-            step(C0{}, STEADY{}, t, sa, sb, mx);
-            step(C1{}, NEXTLASTK{}, t + 1, sb, sa, mx);
-        }
-        if (ntiles - t == 2) {  // t is even here
-            step(C0{}, NEXTLAST{}, t, sa, sb, mx);
-            step(C1{}, LAST{}, t + 1, sb, sa, mx);
-        } else {
-            step(C0{}, LAST{}, t, sa, sb, mx);
-        }
-    }
-
-    FA_STAMP(3);
-    // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (i&3) + 8*(i>>2) + 4*hf
-    // store v * scale as one 16-bit output row (row base Oh)
-    auto store_row = [&](unsigned short* Oh, const f32x16 (&v)[NDB], float scale) {
-#if FA_WIDE_STORE
-        // Column groups g and g+1 of a row sit in lanes l (cols 8g..+3, 8g+8..+11) and
-        // l+32 (8g+4..+7, 8g+12..+15); one v_permlane32_swap per dword leaves 16
-        // contiguous bytes in each lane -> one dwordx4 store per pair instead of two
-        // dwordx2 (cdna_hip_programming.md T21).
-#pragma unroll
-        for (int db = 0; db < NDB; ++db)
-#pragma unroll
-            for (int gp = 0; gp < 4; gp += 2) {
-                unsigned x0 = pack2<T>(v[db][4 * gp + 0] * scale, v[db][4 * gp + 1] * scale);
-                unsigned x1 = pack2<T>(v[db][4 * gp + 2] * scale, v[db][4 * gp + 3] * scale);
-                unsigned y0 = pack2<T>(v[db][4 * gp + 4] * scale, v[db][4 * gp + 5] * scale);
-                unsigned y1 = pack2<T>(v[db][4 * gp + 6] * scale, v[db][4 * gp + 7] * scale);
-                const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-                const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-                const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
-                *(u32x4*)(Oh + db * 32 + 8 * gp + 8 * hf) = u;
-            }
-#else
-#pragma unroll
-        for (int db = 0; db < NDB; ++db)
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                u32x2 u;
-                u[0] = pack2<T>(v[db][4 * g4 + 0] * scale, v[db][4 * g4 + 1] * scale);
-                u[1] = pack2<T>(v[db][4 * g4 + 2] * scale, v[db][4 * g4 + 3] * scale);
-                *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
-            }
-#endif
-    };
-
-    if constexpr (MODE == kFused) {
-        // Split-KV partials combined on chip.  Every workgroup stores its normalised partial
-        // O (PT) and lse in FRAGMENT order -- lane-linear 16-byte pieces, so both the stores
-        // and the combine's loads are fully coalesced -- then counts itself in its query
-        // tile's counter; the workgroup that arrives last reads the other splits' partials
-        // (just written: served by L2 / Infinity Cache) and writes O.  Hand-off protocol
-        // (MI355X_MICROARCH.md, inter-workgroup visibility, first table row): all partial
-        // stores and loads sc1; every wave waits vmcnt(0) after its stores; a barrier; ONE
-        // lane's agent-scope atomic add; the adder that saw count nsplit-1 tells the other
-        // waves through LDS behind a barrier.  No workgroup ever waits for another.
-        constexpr int SC1 = 16;                    // cache-policy bit: sc1
-        constexpr int NF = NDB * 4;                // fragments (4 values) per lane and row block
-        constexpr int BLK = kBQ * D;               // partial elements per (split, tile) block
-        const int64_t grp = bh * a.nqt + qt;
-        auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
-        auto o_rsrc = [&](int sp) {
-            return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, (int64_t)BLK * sizeof(PT));
-        };
-        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
-        auto frag_off = [&](int r, int f) {  // byte offset of fragment f of row block r
-            return ((((wid * RB + r) * NF + f) * 64 + lane) * 4) * (int)sizeof(PT);
-        };
-        const int lse_off = (wid * RB) * 32 * 4 + l32 * 4;  // + r*128
-
-        float inv[RB], lse_own[RB];
-        {
-            const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
-#pragma unroll
-            for (int r = 0; r < RB; ++r) {
-                const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
-                inv[r] = 1.f / l_tot;
-                lse_own[r] = m[r] + __builtin_amdgcn_logf(l_tot);
-#pragma unroll
-                for (int f = 0; f < NF; ++f) {
-                    const int db = f >> 2, g4 = f & 3;
-                    const f32x4 src = {o[r][db][4 * g4], o[r][db][4 * g4 + 1], o[r][db][4 * g4 + 2],
-                                       o[r][db][4 * g4 + 3]};
-                    if constexpr (sizeof(PT) == 4) {
-                        const u32x4 u = {__float_as_uint(src[0] * inv[r]), __float_as_uint(src[1] * inv[r]),
-                                         __float_as_uint(src[2] * inv[r]), __float_as_uint(src[3] * inv[r])};
-                        __builtin_amdgcn_raw_buffer_store_b128(u, ors, frag_off(r, f), 0, SC1);
-                    } else {
-                        const u32x2 u = {pack2<T>(src[0] * inv[r], src[1] * inv[r]),
-                                         pack2<T>(src[2] * inv[r], src[3] * inv[r])};
-                        __builtin_amdgcn_raw_buffer_store_b64(u, ors, frag_off(r, f), 0, SC1);
-                    }
-                }
-                if (hf == 0)
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse_own[r]), lrs, lse_off + r * 128, 0, SC1);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int* const last_flag = (int*)smem;  // LDS is free: the KV loop ended with a barrier
-        if (tid == 0) {
-            const unsigned old = __hip_atomic_fetch_add(a.counters + grp, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old + 1 == (unsigned)a.nsplit;
-            if (last) a.counters[grp] = 0;  // leave the counter zero for the next launch
-            *last_flag = last;
-        }
-        __syncthreads();
-        if (!*last_flag) return;
-
-        // Sum in split order 0, 1, ... whatever workgroup came last (its own partial is read
-        // back too), so that O is bitwise repeatable.
-        const int ns = a.nsplit;
-        auto load_lse = [&](int sp, int r) {
-            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off + r * 128, 0, SC1));
-        };
-        typedef unsigned frag_t __attribute__((ext_vector_type(sizeof(PT))));  // 4 x PT
-        auto load_frags = [&](int sp, int r, frag_t (&dst)[NF]) {
-            const __amdgpu_buffer_rsrc_t rs = o_rsrc(sp);
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                if constexpr (sizeof(PT) == 4)
-                    dst[f] = __builtin_bit_cast(frag_t, __builtin_amdgcn_raw_buffer_load_b128(rs, frag_off(r, f), 0, SC1));
-                else
-                    dst[f] = __builtin_bit_cast(frag_t, __builtin_amdgcn_raw_buffer_load_b64(rs, frag_off(r, f), 0, SC1));
-            }
-        };
-        auto unpack = [](const frag_t& u, int j) -> float {
-            if constexpr (sizeof(PT) == 4) {
-                return __uint_as_float(u[j]);
-            } else {
-                const unsigned w = u[j >> 1];
-                const unsigned short h = (unsigned short)((j & 1) ? (w >> 16) : (w & 0xffff));
-                return (float)__builtin_bit_cast(T, h);
-            }
-        };
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            float M = lse_own[r];
-            for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, load_lse(sp, r));
-            float wsum = 0.f;
-            f32x16 acc[NDB];
-#pragma unroll
-            for (int db = 0; db < NDB; ++db) acc[db] = f32x16{};
-            auto fma_split = [&](const frag_t (&fr)[NF], float w) {
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[f >> 2][4 * (f & 3) + j] = __builtin_fmaf(w, unpack(fr[f], j), acc[f >> 2][4 * (f & 3) + j]);
-                wsum += w;
-            };
-            // two splits in flight: the loads of split sp+1 overlap the FMAs of split sp
-            frag_t fa_[NF], fb_[NF];
-            float wa, wb = 0.f;
-            load_frags(0, r, fa_);
-            wa = __builtin_amdgcn_exp2f(load_lse(0, r) - M);
-            for (int sp = 0; sp < ns; sp += 2) {
-                if (sp + 1 < ns) {
-                    load_frags(sp + 1, r, fb_);
-                    wb = __builtin_amdgcn_exp2f(load_lse(sp + 1, r) - M);
-                }
-                fma_split(fa_, wa);
-                if (sp + 1 < ns) {
-                    if (sp + 2 < ns) {
-                        load_frags(sp + 2, r, fa_);
-                        wa = __builtin_amdgcn_exp2f(load_lse(sp + 2, r) - M);
-                    }
-                    fma_split(fb_, wb);
-                }
-            }
-            const int64_t q_row = q_row0 + 32 * r;
-            if (q_row < a.Lq)
-                store_row((unsigned short*)a.o_final + bh * a.Lq * D + q_row * D, acc, 1.f / wsum);
-        }
-    } else {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-        const int64_t q_row = q_row0 + 32 * r;
-        const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
-        const float inv = 1.f / l_tot;
-        if (q_row >= a.Lq) continue;
-        if constexpr (MODE == kFinal) {
-            store_row((unsigned short*)a.o + bh * a.Lq * D + q_row * D, o[r], inv);
-        } else {
-            const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
-            const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
-            PT* Op = (PT*)a.o + split * a.split_stride + row_lin * D;
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const int col = db * 32 + 8 * g4 + 4 * hf;
-                    if constexpr (sizeof(PT) == 4) {
-                        f32x4 f = {o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv,
-                                   o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv};
-                        *(f32x4*)(Op + col) = f;
-                    } else {
-                        u32x2 u;
-                        u[0] = pack2<T>(o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv);
-                        u[1] = pack2<T>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
-                        *(u32x2*)((unsigned short*)Op + col) = u;
-                    }
-                }
-            // lse in log2 units: m + log2(l)  (v_log_f32 is log2)
-            if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m[r] + __builtin_amdgcn_logf(l_tot);
-        }
-    }
-    }
-#if FA_STAMPS
-    FA_STAMP(4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FA_STAMP(5);
-    FA_STAMP_V(9, __builtin_amdgcn_s_memrealtime());
-#endif
-}
 
 int fwd_lds_bytes(int d) { return 2 * 2 * bk_for(d) * d * 2; }
 
@@ -785,6 +33,7 @@ static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s) {
+    if (a.strided) return launch_fwd_strided(t, pt, d, mode, a, s);
     if (FA_W64 && mode == kFinal && d == 128) return launch_fwd_w64(t, a, s);
     if (FA_PERSIST && mode == kFinal && d <= 128) return launch_fwd_persist(t, d, a, s);
     if (mode == kFinal) {

@@ -72,6 +72,12 @@ struct FwdArgs {
     double scale_log2_64;    // log2(e) / sqrt(d) in double
     double* lse64;           // partial only: log2-sum-exp per row (double)
     unsigned sched_epoch;    // persistent kernel: selects its work-queue set (fa_fwd_persist.hip)
+    // strided tensors (final and fused split modes of fa_fwd_kernel): element strides of
+    // (batch, head, row); d is contiguous and V shares K's strides.  strided == 0: contiguous
+    // [B, H, L, d] and these are unused.
+    int strided;
+    int64_t H;
+    int64_t q_stride[3], k_stride[3], o_stride[3];
 };
 
 // Kernel modes: one workgroup per (query tile, split, b*h) in all three.
@@ -93,6 +99,8 @@ struct CombineArgs {
 // Launchers (defined in the .hip files).  Return hipSuccess or the launch error.
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStream_t s);
+// the strided instantiations (fa_fwd_strided.hip); launch_fwd forwards there when a.strided
+hipError_t launch_fwd_strided(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
 // d = 128 final mode with 64 rows per wave (fa_fwd_w64.hip); FA_W64 selects it
 #ifndef FA_W64

@@ -1,6 +1,8 @@
 """Device-tensor operators over the C ABI (torch tensors in HBM, zero-copy).
 
-Every function takes contiguous ``[B, H, L, d]`` bf16 / fp16 tensors on a ROCm device,
+Every function takes ``[B, H, L, d]`` bf16 / fp16 (or fp64) tensors on a ROCm device --
+contiguous, or for attention_v1 / _tiled_d / _v2 any view with a contiguous d (strided
+kernels, no copy) --
 launches on the current HIP stream of that device and returns without synchronising.
 PyTorch is only the plumbing here (device memory, streams); the work is done by the
 gfx950 kernels in libfa_mi355x.so.
@@ -65,7 +67,34 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _check_tensor(name, t, dtype=None, device=None, ndim=4):
+def _stride_args(q, k, v, o):
+    """Stride arguments of the *_ex entry points for a mix of contiguous and strided
+    [B, H, L, d] tensors: None when all four are contiguous, False when some view is not
+    expressible (d not contiguous, strides not multiples of 8 elements, k and v strided
+    differently, fp64), else three ctypes int64[3] arrays {batch, head, row} for q, k/v, o."""
+    ts = (q, k, v, o)
+    if all(t.is_contiguous() for t in ts):
+        return None
+    if q.dtype not in (torch.bfloat16, torch.float16) or k.stride() != v.stride():
+        return False
+
+    def ok(t):
+        st = t.stride()
+        return (st[3] == 1 and all(x > 0 and x % 8 == 0 for x in st[:3]) and st[2] >= t.shape[3]
+                and t.data_ptr() % 16 == 0)
+
+    if not all(ok(t) for t in ts):
+        return False
+    return tuple((ctypes.c_int64 * 3)(*t.stride()[:3]) for t in (q, k, o))
+
+
+def _via_contiguous(fn, q, k, v, o, **kw):
+    """Run fn on contiguous copies of views the strided kernels cannot address."""
+    o.copy_(fn(q.contiguous(), k.contiguous(), v.contiguous(), **kw))
+    return o
+
+
+def _check_tensor(name, t, dtype=None, device=None, ndim=4, strided=False):
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
     if t.device.type != "cuda":
@@ -73,7 +102,7 @@ def _check_tensor(name, t, dtype=None, device=None, ndim=4):
                          "the MI355X path has no CPU fallback")
     if t.dim() != ndim:
         raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
-    if not t.is_contiguous():
+    if not strided and not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
     if dtype is not None and t.dtype != dtype:
         raise ValueError(f"{name} has dtype {t.dtype}, expected {dtype}")
@@ -81,12 +110,12 @@ def _check_tensor(name, t, dtype=None, device=None, ndim=4):
         raise ValueError(f"{name} is on {t.device}, expected {device}")
 
 
-def _check_qkv(q, k, v, same_len=True):
-    _check_tensor("q", q)
+def _check_qkv(q, k, v, same_len=True, strided=False):
+    _check_tensor("q", q, strided=strided)
     if q.dtype not in _DTYPES:
         raise ValueError(f"q dtype {q.dtype} unsupported (bfloat16, float16 or float64)")
-    _check_tensor("k", k, q.dtype, q.device)
-    _check_tensor("v", v, q.dtype, q.device)
+    _check_tensor("k", k, q.dtype, q.device, strided=strided)
+    _check_tensor("v", v, q.dtype, q.device, strided=strided)
     if k.shape != v.shape:
         raise ValueError(f"k {tuple(k.shape)} and v {tuple(v.shape)} must have the same shape")
     if q.shape[0] != k.shape[0] or q.shape[1] != k.shape[1] or q.shape[3] != k.shape[3]:
@@ -95,12 +124,12 @@ def _check_qkv(q, k, v, same_len=True):
         raise ValueError(f"q {tuple(q.shape)} and k {tuple(k.shape)} must have the same shape")
 
 
-def _out(out, q, shape=None, dtype=None):
+def _out(out, q, shape=None, dtype=None, strided=False):
     shape = tuple(q.shape) if shape is None else shape
     dtype = q.dtype if dtype is None else dtype
     if out is None:
         return torch.empty(shape, dtype=dtype, device=q.device)
-    _check_tensor("out", out, dtype, q.device, ndim=len(shape))
+    _check_tensor("out", out, dtype, q.device, ndim=len(shape), strided=strided)
     if tuple(out.shape) != shape:
         raise ValueError(f"out has shape {tuple(out.shape)}, expected {shape}")
     return out
@@ -108,13 +137,22 @@ def _out(out, q, shape=None, dtype=None):
 
 def attention_v1(q, k, v, out=None):
     """FA-v1 fused forward: O = softmax(q k^T / sqrt(d)) v.  Any 1 <= d <= 256 (head dims
-    without a kernel are zero-padded to the next one, see kernel_head_dim)."""
-    _check_qkv(q, k, v)
-    o = _out(out, q)
+    without a kernel are zero-padded to the next one, see kernel_head_dim).  q, k, v and out
+    may be strided [B, H, L, d] views with a contiguous d -- e.g. ``x.transpose(1, 2)`` of a
+    [B, L, H, d] tensor -- which the kernel addresses in place (fa_fwd_v1_ex)."""
+    _check_qkv(q, k, v, strided=True)
+    o = _out(out, q, strided=True)
     B, H, L, d = q.shape
     D = kernel_head_dim(d)
+    st = _stride_args(q, k, v, o) if D == d else None
+    if st is False:
+        return _via_contiguous(attention_v1, q, k, v, o)
     if D == d:
-        check(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
+        if st is None:
+            check(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
+        else:
+            check(lib().fa_fwd_v1_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, st[0], st[1], st[2],
+                                     1.0 / d ** 0.5, _DTYPES[q.dtype], _stream(q)))
         return o
     qp, kp, vp = (_pad_d(t, D) for t in (q, k, v))
     op = torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
@@ -141,11 +179,13 @@ def _d_tiles(d, d_tile_qk, d_tile_v):
 def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
     """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher
     (0 < d_tile <= d; default min(32, d))."""
-    _check_qkv(q, k, v)
+    _check_qkv(q, k, v, strided=True)
     B, H, L, d = q.shape
     d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
-    if kernel_head_dim(d) != d:
-        # the tile arguments are validated against the true d, as the launcher does
+    if kernel_head_dim(d) != d or not all(t.is_contiguous() for t in (q, k, v)) or (
+            out is not None and not out.is_contiguous()):
+        # padded head dims and strided views run on fa_fwd_v1's paths (the same kernel); the
+        # tile arguments are validated against the true d, as the launcher does
         # (flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327)
         for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
             if not 0 < int(t) <= d:
@@ -187,11 +227,16 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
     ``workspace`` (a uint8 device tensor) is allocated from torch's caching allocator when
     not given, so the call itself never reaches hipMalloc after warm-up.
     """
-    _check_qkv(q, k, v)
-    o = _out(out, q)
+    _check_qkv(q, k, v, strided=True)
+    o = _out(out, q, strided=True)
     B, H, L, d = q.shape
     D = kernel_head_dim(d)
     d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
+    st = _stride_args(q, k, v, o) if D == d else None
+    if st is False:
+        return _via_contiguous(attention_v2, q, k, v, o, kv_tiles_per_block=kv_tiles_per_block,
+                               d_tile_qk=d_tile_qk, d_tile_v=d_tile_v, partial_dtype=partial_dtype,
+                               workspace=workspace)
     pd = _default_pdtype(q.dtype, partial_dtype)
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
@@ -200,10 +245,15 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
     elif workspace.numel() * workspace.element_size() < nbytes:
         raise ValueError(f"workspace too small: {nbytes} bytes needed")
     wsb = workspace.numel() * workspace.element_size()
-    if D == d:
+    if D == d and st is None:
         check(lib().fa_fwd_v2(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
                               int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb,
                               _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
+        return o
+    if D == d:
+        check(lib().fa_fwd_v2_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+                                 int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb, st[0], st[1],
+                                 st[2], 1.0 / d ** 0.5, _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
         return o
     for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
         if not 0 < int(t) <= d:

@@ -95,6 +95,16 @@ int fa_fwd_v1(const void* q, const void* k, const void* v, void* o,
 int fa_fwd_v1_scaled(const void* q, const void* k, const void* v, void* o,
                      int64_t B, int64_t H, int64_t L, int64_t d, double softmax_scale,
                      int dtype, void* stream);
+/* fa_fwd_v1_scaled on strided tensors.  q_strides, kv_strides (shared by k and v) and
+ * o_strides each point to three element strides {batch, head, row} of a [B, H, L, d] view
+ * whose d is contiguous -- e.g. a [B, L, H, d] tensor is {L*H*d, d, H*d} -- or are NULL for
+ * contiguous [B, H, L, d].  Strides must be positive multiples of 8 elements (16-byte row
+ * starts), row strides >= d, and one head's rows must span < 2 GiB; bf16 / fp16 only
+ * (FA_DTYPE_FP64 with strides: FA_ERR_UNSUPPORTED).  No copy is made. */
+int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o,
+                 int64_t B, int64_t H, int64_t L, int64_t d,
+                 const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
+                 double softmax_scale, int dtype, void* stream);
 /* FA-v1 d-tiled forward.  d_tile_qk / d_tile_v must satisfy 0 < d_tile <= d
  * (the reference's asserts, flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327),
  * otherwise FA_ERR_INVALID_ARG.  The d-chunking of the arithmetic is set by the MFMA
@@ -145,6 +155,13 @@ int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o,
                      int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
                      void* workspace, size_t workspace_bytes, double softmax_scale,
                      int dtype, int partial_dtype, void* stream);
+/* fa_fwd_v2_scaled on strided q, k, v, o (strides as for fa_fwd_v1_ex). */
+int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o,
+                 int64_t B, int64_t H, int64_t L, int64_t d,
+                 int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
+                 void* workspace, size_t workspace_bytes,
+                 const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
+                 double softmax_scale, int dtype, int partial_dtype, void* stream);
 /* Split-KV partial forward over ONE key range (a whole KV shard, e.g. one GPU's
  * slice of the sequence).  q: [B, H, Lq, d]; k, v: [B, H, Lk, d].
  * Writes, for every query row, the normalised partial output and its log-sum-exp

@@ -90,6 +90,22 @@ def test_scaled_entry_points_validate_scale():
     assert st != L.FA_OK
 
 
+def test_strided_entry_points_validate_strides():
+    lib = L.lib()
+    fake = ctypes.c_void_p(0x10000)
+    S = ctypes.c_int64 * 3
+    good = S(4 * 64 * 128, 128, 4 * 128)  # [B, L=64, H=4, d=128] viewed as [B, H, L, d]
+    args = (fake, fake, fake, fake, 1, 4, 64, 128)
+    for bad in (S(0, 128, 512), S(32768, 128, 100), S(32768, 128, 64), S(-8, 128, 512)):
+        st = lib.fa_fwd_v1_ex(*args, bad, good, good, 0.1, L.FA_DTYPE_BF16, NULL)
+        assert st == L.FA_ERR_INVALID_ARG and b"stride" in lib.fa_last_error(), bytes(lib.fa_last_error())
+    st = lib.fa_fwd_v1_ex(*args, good, good, good, 0.1, L.FA_DTYPE_FP64, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED
+    huge = S(1 << 40, 128, 1 << 25)  # rows of one head span > 2 GiB
+    st = lib.fa_fwd_v1_ex(*args, huge, good, good, 0.1, L.FA_DTYPE_BF16, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED
+
+
 def test_kernel_head_dim_padding_map():
     from exploring_flash_attention_amd import ops
     assert [ops.kernel_head_dim(d) for d in (1, 16, 32, 33, 48, 64, 80, 96, 128, 129, 200, 256)] == \

@@ -199,6 +199,46 @@ def test_head_dims_without_a_kernel(gpu, d):
             assert np.abs(o64 - ref).max() <= 1e-12
 
 
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+def test_strided_bshd_views(gpu, d):
+    """[B, L, H, d] tensors passed as [B, H, L, d] views (x.transpose(1, 2)): the strided
+    kernels address them in place (fa_fwd_v1_ex / fa_fwd_v2_ex), output written into a
+    [B, L, H, d] buffer through its view; every variant against the fp64 oracle."""
+    from exploring_flash_attention_amd import ops
+    for i, (B, H, L) in enumerate([(2, 3, 200), (1, 4, 256)]):
+        q, k, v = _inputs(B, H, L, d, torch.bfloat16, seed=20 + i)
+        ref = _ref(q, k, v)
+        qs, ks, vs = (x.transpose(1, 2).contiguous().to(gpu).transpose(1, 2) for x in (q, k, v))
+        assert not qs.is_contiguous() and qs.stride()[3] == 1
+        for name, fn in (("v1", lambda a, b, c, o: ops.attention_v1(a, b, c, out=o)),
+                         ("tiled_d", lambda a, b, c, o: ops.attention_tiled_d(a, b, c, 32, 32, out=o)),
+                         ("v2_1", lambda a, b, c, o: ops.attention_v2(a, b, c, 1, out=o)),
+                         ("v2_4", lambda a, b, c, o: ops.attention_v2(a, b, c, 4, out=o))):
+            o_bshd = torch.full((B, L, H, d), float("nan"), dtype=torch.bfloat16, device=gpu)
+            out = fn(qs, ks, vs, o_bshd.transpose(1, 2))
+            torch.cuda.synchronize()
+            assert out.data_ptr() == o_bshd.data_ptr(), name
+            _gate(o_bshd.transpose(1, 2).contiguous(), ref, torch.bfloat16)
+        # mixed: strided q, contiguous k / v, contiguous result
+        o = ops.attention_v1(qs, k.to(gpu), v.to(gpu))
+        _gate(o, ref, torch.bfloat16)
+
+
+def test_strided_views_without_kernel_layout(gpu):
+    """Views the strided kernels cannot take (d not contiguous, k and v strided differently,
+    fp64) run on contiguous copies: same results, out written in place."""
+    from exploring_flash_attention_amd import ops
+    B, H, L, d = 1, 2, 130, 64
+    q, k, v = _inputs(B, H, L, d, torch.bfloat16, seed=31)
+    ref = _ref(q, k, v)
+    qt = q.transpose(2, 3).contiguous().to(gpu).transpose(2, 3)  # d strided by L
+    kd, vd = k.to(gpu), v.transpose(1, 2).contiguous().to(gpu).transpose(1, 2)
+    for fn in (ops.attention_v1, lambda a, b, c: ops.attention_v2(a, b, c, 1)):
+        _gate(fn(qt, kd, vd), ref, torch.bfloat16)
+    q64, k64, v64 = (x.double().transpose(1, 2).contiguous().to(gpu).transpose(1, 2) for x in (q, k, v))
+    assert np.abs(ops.attention_v1(q64, k64, v64).cpu().numpy() - ref).max() <= 1e-12
+
+
 def test_golden_flat_surface_d16(gpu):
     """The reference's own d = 16 case (numpy_gpu_like_opt2.py surface, L = 40): fp64 in,
     fp64 kernel on the zero-padded d = 32, 1e-12 against the reference's output."""
