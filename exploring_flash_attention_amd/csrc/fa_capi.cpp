@@ -127,7 +127,7 @@ int apply_strides(fa::FwdArgs& a, fa::Elem e, int64_t B, int64_t H, int64_t L, i
         }
         if (st[t][2] < d)
             return fail(FA_ERR_INVALID_ARG, "%s row stride %lld < d=%lld", names[t], (long long)st[t][2], (long long)d);
-        if ((L - 1) * st[t][2] * 2 + d * 2 > 0x7fffffffLL)
+        if (st[t][2] > (int64_t)1 << 28 || (L - 1) * st[t][2] * 2 + d * 2 > 0x7fffffffLL)
             return fail(FA_ERR_UNSUPPORTED, "%s: one head's rows span more than 2 GiB", names[t]);
         (void)B;
     }

@@ -193,8 +193,12 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     const int64_t k_head = STRIDED ? hb * a.k_stride[0] + hh * a.k_stride[1] : bh * a.Lk * D;
     // Buffer descriptors: K/V cover exactly this split's keys, so the DMA of the last
     // (partial) tile reads zeros past kv_end with no clamping code.
-    const unsigned short* Qh = (const unsigned short*)a.q + q_head;
-    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, STRIDED ? (a.Lq - 1) * qrb + ROWB : a.Lq * ROWB);
+    // Q descriptor over this workgroup's query tile only, so that its 32-bit offsets stay
+    // small however long the sequence (rows past Lq read zeros)
+    const int64_t q_tile0 = (int64_t)qt * kBQ;
+    const unsigned short* Qh = (const unsigned short*)a.q + q_head + q_tile0 * (qrb / 2);
+    const int64_t q_rows = a.Lq - q_tile0 < kBQ ? a.Lq - q_tile0 : kBQ;
+    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, STRIDED ? (q_rows - 1) * qrb + ROWB : q_rows * ROWB);
     // K/V of this split; a tile's descriptor (made per DMA, scalar arithmetic only) starts
     // at the tile and ends at the split's last key, so the hardware range check -- which
     // does not rely on soffset -- zero-fills the rows of a partial last tile.
@@ -203,11 +207,11 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 
     // Q^T fragments (B operand): lane holds Q[row][16*ks + 8*hf + 0..7] of each of its
     // RB row blocks.  Rows past Lq read zeros and are never stored.
-    const int64_t q_row0 = (int64_t)qt * kBQ + wid * kRowsPerWave + l32;
+    const int64_t q_row0 = q_tile0 + wid * kRowsPerWave + l32;
     v8 qf[RB][NKS];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-        const int qoff = (int)((q_row0 + 32 * r) * qrb) + hf * 16;
+        const int qoff = (wid * kRowsPerWave + l32 + 32 * r) * qrb + hf * 16;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
             qf[r][ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, qoff + ks * 32, 0, 0));
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         // (strided rows: the range ends at the last valid row's end)
         const int bytes = STRIDED ? (valid > 0 ? (valid - 1) * krb + ROWB : 0) : valid * ROWB;
         const __amdgpu_buffer_rsrc_t rs =
-            make_rsrc32((const char*)base + (int64_t)t * (STRIDED ? kBK * krb : TILEB), bytes);
+            make_rsrc32((const char*)base + (int64_t)t * (STRIDED ? (int64_t)kBK * krb : (int64_t)TILEB), bytes);
 #else
         const int64_t off = (int64_t)t * TILEB;
         const int64_t kv_bytes = (int64_t)nkv * ROWB;

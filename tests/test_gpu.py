@@ -375,6 +375,28 @@ def test_long_sequence_sampled_rows(gpu):
             assert m["max_abs"] < 6e-3, m
 
 
+def test_query_rows_beyond_2gib(gpu):
+    """One head whose Q spans more than 2 GiB (Lq = 2^23 + 64 rows of d = 128): every
+    workgroup's Q buffer range starts at its own tile, so the 32-bit buffer offsets never
+    overflow.  Through the partial entry point (Lq != Lk keeps the work small); sampled rows
+    against the oracle."""
+    from exploring_flash_attention_amd import ops
+    Lq, Lk, d = (1 << 23) + 64, 64, 128
+    g = torch.Generator(device=gpu).manual_seed(3)
+    q = torch.randn(1, 1, Lq, d, device=gpu, dtype=torch.bfloat16, generator=g)
+    k, v = (torch.randn(1, 1, Lk, d, device=gpu, dtype=torch.bfloat16, generator=g) for _ in range(2))
+    assert q.numel() * 2 > 2 ** 31
+    o_part, lse = ops.attention_partial(q, k, v)
+    torch.cuda.synchronize()
+    rows = torch.tensor([0, 1, (1 << 22) + 5, (1 << 23) - 1, (1 << 23), Lq - 1], device=gpu)
+    ref = attention_fp64(q[0, 0, rows].double().cpu().numpy(), k[0, 0].double().cpu().numpy(),
+                         v[0, 0].double().cpu().numpy())
+    got = o_part[0, 0, rows].float().cpu().numpy()
+    assert accuracy_metrics(got, ref)["max_abs"] < 6e-3
+    del q, o_part, lse
+    torch.cuda.empty_cache()
+
+
 def test_runs_on_side_stream(gpu):
     from exploring_flash_attention_amd import ops
     q, k, v = _inputs(1, 2, 256, 64, torch.float16, seed=1)
