@@ -144,6 +144,8 @@ def attention_v1(q, k, v, out=None):
     o = _out(out, q, strided=True)
     B, H, L, d = q.shape
     D = kernel_head_dim(d)
+    if q.numel() == 0:  # no rows: nothing to launch (the reference returns an empty O)
+        return o
     st = _stride_args(q, k, v, o) if D == d else None
     if st is False:
         return _via_contiguous(attention_v1, q, k, v, o)
@@ -182,7 +184,7 @@ def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
     _check_qkv(q, k, v, strided=True)
     B, H, L, d = q.shape
     d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
-    if kernel_head_dim(d) != d or not all(t.is_contiguous() for t in (q, k, v)) or (
+    if q.numel() == 0 or kernel_head_dim(d) != d or not all(t.is_contiguous() for t in (q, k, v)) or (
             out is not None and not out.is_contiguous()):
         # padded head dims and strided views run on fa_fwd_v1's paths (the same kernel); the
         # tile arguments are validated against the true d, as the launcher does
@@ -232,6 +234,8 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
     B, H, L, d = q.shape
     D = kernel_head_dim(d)
     d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
+    if q.numel() == 0:  # no rows: nothing to launch
+        return o
     st = _stride_args(q, k, v, o) if D == d else None
     if st is False:
         return _via_contiguous(attention_v2, q, k, v, o, kv_tiles_per_block=kv_tiles_per_block,

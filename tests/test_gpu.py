@@ -239,6 +239,24 @@ def test_strided_views_without_kernel_layout(gpu):
     assert np.abs(ops.attention_v1(q64, k64, v64).cpu().numpy() - ref).max() <= 1e-12
 
 
+def test_empty_inputs(gpu):
+    """L = 0 (and B = 0): the reference's NumPy functions return an empty O
+    (flash_attention_v1/numpy_basic.py:79-103 never enters its loops); so do these, without
+    a launch."""
+    import exploring_flash_attention_amd as fa
+    from exploring_flash_attention_amd import ops, v1
+    for shape in ((1, 2, 0, 64), (0, 2, 16, 128), (1, 1, 0, 48)):
+        q = torch.empty(shape, dtype=torch.bfloat16, device=gpu)
+        for fn in (ops.attention_v1, lambda a, b, c: ops.attention_tiled_d(a, b, c),
+                   lambda a, b, c: ops.attention_v2(a, b, c, 1)):
+            o = fn(q, q, q)
+            assert tuple(o.shape) == shape and o.dtype == torch.bfloat16
+    Z = np.zeros((0, 32))
+    O = v1.flash_attention_tiled(Z, Z, Z)
+    assert O.shape == (0, 32) and O.dtype == np.float64
+    assert fa.flash_attention_v1(Z, Z, Z).shape == (0, 32)
+
+
 def test_golden_flat_surface_d16(gpu):
     """The reference's own d = 16 case (numpy_gpu_like_opt2.py surface, L = 40): fp64 in,
     fp64 kernel on the zero-padded d = 32, 1e-12 against the reference's output."""
