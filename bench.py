@@ -19,12 +19,14 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md)
+C5_TIMEOUT_S = 240  # watchdog of the C5 split-KV extra (seconds)
 CONFIGS = {
     "c2": dict(B=32, H=8, L=1024, d=32, variant="v1"),
     "c3": dict(B=32, H=8, L=1024, d=128, variant="v1"),
@@ -222,23 +224,6 @@ def main():
     total_work = work * world
     value = total_work / (wall / args.steps) / 1e9
 
-    if not args.no_extra and args.mode == "heads":
-        # C5 split-KV over all ranks (north_star: 1/2/4/8-GPU split-KV throughput and achieved
-        # fraction); every rank takes part in the exchange, time = max over ranks
-        st5, _, w5 = c5_step(torch, fdist, dev, world, rank)
-        n5 = 10
-        wall5, ems5 = time_step(torch, st5, n5, 3, barrier)
-        t5 = torch.tensor([wall5, ems5], device=dev, dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(t5, op=dist.ReduceOp.MAX)
-        ms5 = float(t5[0]) / n5 * 1e3
-        tf5 = w5 * world / (ms5 * 1e-3) / 1e12
-        extra["c5_splitkv_dist"] = {"ms": round(ms5, 3), "tflops": round(tf5, 1),
-                                    "frac": round(tf5 / (PEAK_BF16_TFLOPS * world), 4), "ranks": world,
-                                    "exchange": "all_to_all_single (RCCL)" if world > 1 else "none"}
-        del st5
-        torch.cuda.empty_cache()
-
     if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
         # per-variant timings at N=1 (informational; not the headline value)
         for name, c, fn in (("c3_tiled_d", "c3", "tiled_d"), ("c2_fused", "c2", "v1"),
@@ -293,11 +278,48 @@ def main():
                          "kernel_ms": round(avg_ms, 5)},
             "cpu_baseline": cpu,
         }
+    printed, dog = False, None
+    if not args.no_extra and args.mode == "heads":
+        # C5 split-KV over all ranks (north_star: 1/2/4/8-GPU split-KV throughput and achieved
+        # fraction); every rank takes part in the exchange, time = max over ranks.  A watchdog
+        # keeps an exchange that never completes from costing the headline line: after
+        # C5_TIMEOUT_S every rank leaves, rank 0 printing what was measured.
+        def _give_up():
+            if rank == 0 and not printed:
+                extra["c5_splitkv_dist"] = {"error": f"no result within {C5_TIMEOUT_S} s", "ranks": world}
+                line["extra"] = extra
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+        dog = threading.Timer(C5_TIMEOUT_S, _give_up)
+        dog.daemon = True
+        dog.start()
+        try:
+            st5, _, w5 = c5_step(torch, fdist, dev, world, rank)
+            n5 = 10
+            wall5, ems5 = time_step(torch, st5, n5, 3, barrier)
+            t5 = torch.tensor([wall5, ems5], device=dev, dtype=torch.float64)
+            if world > 1:
+                dist.all_reduce(t5, op=dist.ReduceOp.MAX)
+            ms5 = float(t5[0]) / n5 * 1e3
+            tf5 = w5 * world / (ms5 * 1e-3) / 1e12
+            extra["c5_splitkv_dist"] = {"ms": round(ms5, 3), "tflops": round(tf5, 1),
+                                        "frac": round(tf5 / (PEAK_BF16_TFLOPS * world), 4), "ranks": world,
+                                        "exchange": ("per-chunk partials pipelined with pairwise RCCL "
+                                                     "send/recv" if world > 1 else "none")}
+            del st5
+        except Exception as exc:  # noqa: BLE001 -- reported, the headline stands
+            extra["c5_splitkv_dist"] = {"error": f"{type(exc).__name__}: {exc}"[:300], "ranks": world}
+        torch.cuda.empty_cache()
+
+    if rank == 0:
         if extra:
             line["extra"] = extra
         print(json.dumps(line), flush=True)
+        printed = True
     if world > 1:
         dist.destroy_process_group()
+    if dog is not None:
+        dog.cancel()
 
 
 if __name__ == "__main__":

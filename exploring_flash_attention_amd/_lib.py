@@ -48,6 +48,7 @@ SIGNATURES = {
     "fa_fwd_v2_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
                           _P, _P, _P, ctypes.c_double, _I, _I, _P]),
     "fa_fwd_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
+    "fa_fwd_partial_ex": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I, _I, _P]),
     "fa_combine": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
 }
 

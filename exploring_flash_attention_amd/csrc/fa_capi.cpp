@@ -112,13 +112,15 @@ fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int6
 // contiguous).  Every row start must stay 16-byte aligned (the kernel loads 16 B per lane)
 // and one head's rows must span < 2 GiB (32-bit buffer offsets).
 int apply_strides(fa::FwdArgs& a, fa::Elem e, int64_t B, int64_t H, int64_t L, int64_t d,
-                  const int64_t* qs, const int64_t* kvs, const int64_t* os) {
+                  const int64_t* qs, const int64_t* kvs, const int64_t* os, int64_t Lk = -1) {
     a.H = H;
     if (!qs && !kvs && !os) return FA_OK;
     if (e == fa::Elem::F64) return fail(FA_ERR_UNSUPPORTED, "strided tensors: bf16 / fp16 only");
-    const int64_t contig[3] = {H * L * d, L * d, d};
-    const int64_t* st[3] = {qs ? qs : contig, kvs ? kvs : contig, os ? os : contig};
+    if (Lk < 0) Lk = L;
+    const int64_t contig[3] = {H * L * d, L * d, d}, contig_k[3] = {H * Lk * d, Lk * d, d};
+    const int64_t* st[3] = {qs ? qs : contig, kvs ? kvs : contig_k, os ? os : contig};
     const char* names[3] = {"q", "k/v", "o"};
+    const int64_t rows[3] = {L, Lk, L};
     for (int t = 0; t < 3; ++t) {
         for (int i = 0; i < 3; ++i) {
             if (st[t][i] <= 0 || (st[t][i] * 2) % 16)
@@ -127,7 +129,7 @@ int apply_strides(fa::FwdArgs& a, fa::Elem e, int64_t B, int64_t H, int64_t L, i
         }
         if (st[t][2] < d)
             return fail(FA_ERR_INVALID_ARG, "%s row stride %lld < d=%lld", names[t], (long long)st[t][2], (long long)d);
-        if (st[t][2] > (int64_t)1 << 28 || (L - 1) * st[t][2] * 2 + d * 2 > 0x7fffffffLL)
+        if (st[t][2] > (int64_t)1 << 28 || (rows[t] - 1) * st[t][2] * 2 + d * 2 > 0x7fffffffLL)
             return fail(FA_ERR_UNSUPPORTED, "%s: one head's rows span more than 2 GiB", names[t]);
         (void)B;
     }
@@ -391,6 +393,13 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
 int fa_fwd_partial(const void* q, const void* k, const void* v, void* o_part, void* lse,
                    int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d, int64_t chunk_rows,
                    int dtype, int partial_dtype, void* stream) {
+    return fa_fwd_partial_ex(q, k, v, o_part, lse, B, H, Lq, Lk, d, chunk_rows, nullptr, dtype, partial_dtype,
+                             stream);
+}
+
+int fa_fwd_partial_ex(const void* q, const void* k, const void* v, void* o_part, void* lse,
+                      int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d, int64_t chunk_rows,
+                      const int64_t* q_strides, int dtype, int partial_dtype, void* stream) {
     fa::Elem e, pe;
     if (int st = check_shape(B, H, Lq, d)) return st;
     if (Lk <= 0 || Lk > (int64_t)1 << 30)
@@ -407,6 +416,7 @@ int fa_fwd_partial(const void* q, const void* k, const void* v, void* o_part, vo
     a.lse64 = (double*)lse;
     a.chunk_rows = chunk_rows;
     a.split_stride = 0;
+    if (int st = apply_strides(a, e, B, H, Lq, d, q_strides, nullptr, nullptr, Lk)) return st;
     if (hipError_t he = e == fa::Elem::F64
                             ? fa::launch_fwd64((int)d, fa::kPartial, a, (hipStream_t)stream)
                             : fa::launch_fwd(e, pe, (int)d, fa::kPartial, a, (hipStream_t)stream))

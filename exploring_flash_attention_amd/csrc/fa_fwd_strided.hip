@@ -1,7 +1,8 @@
 // fa_fwd_strided.hip -- launchers of the forward kernel (fa_fwd_kernel.hpp) on strided
 // tensors: [B, H, L, d] views with arbitrary (batch, head, row) element strides and a
 // contiguous d, e.g. the [B, L, H, d] layout most frameworks keep, with no copy.  Final mode
-// (FA-v1 fused / d-tiled) and the fused split-KV mode (FA-v2).
+// (FA-v1 fused / d-tiled), the fused split-KV mode (FA-v2) and the row-layout partial mode
+// (fa_fwd_partial_ex: one chunk of query rows per launch in the multi-GPU path).
 #include "fa_fwd_kernel.hpp"
 
 namespace fa {
@@ -36,11 +37,16 @@ hipError_t launch_fwd_strided(Elem t, Elem pt, int d, Mode mode, const FwdArgs& 
         if (t == Elem::F16) return launch_strided_d<_Float16, _Float16, kFinal>(d, a, s);
         return hipErrorInvalidValue;
     }
-    if (mode != kFused) return hipErrorInvalidValue;
-    if (t == Elem::BF16 && pt == Elem::BF16) return launch_strided_d<__bf16, __bf16, kFused>(d, a, s);
-    if (t == Elem::BF16 && pt == Elem::F32) return launch_strided_d<__bf16, float, kFused>(d, a, s);
-    if (t == Elem::F16 && pt == Elem::F16) return launch_strided_d<_Float16, _Float16, kFused>(d, a, s);
-    if (t == Elem::F16 && pt == Elem::F32) return launch_strided_d<_Float16, float, kFused>(d, a, s);
+    auto pick = [&](auto mode_c) -> hipError_t {
+        constexpr int M = decltype(mode_c)::value;
+        if (t == Elem::BF16 && pt == Elem::BF16) return launch_strided_d<__bf16, __bf16, M>(d, a, s);
+        if (t == Elem::BF16 && pt == Elem::F32) return launch_strided_d<__bf16, float, M>(d, a, s);
+        if (t == Elem::F16 && pt == Elem::F16) return launch_strided_d<_Float16, _Float16, M>(d, a, s);
+        if (t == Elem::F16 && pt == Elem::F32) return launch_strided_d<_Float16, float, M>(d, a, s);
+        return hipErrorInvalidValue;
+    };
+    if (mode == kFused) return pick(std::integral_constant<int, kFused>{});
+    if (mode == kPartial) return pick(std::integral_constant<int, kPartial>{});
     return hipErrorInvalidValue;
 }
 

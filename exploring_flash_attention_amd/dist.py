@@ -11,7 +11,9 @@ results of every key shard -- is an all-to-all:
      SEND layout [W][B*H][L/W][d]: chunk j = the query rows rank j will own;
   2. all_to_all_single of O (bf16 by default) and lse (fp32): each rank sends W-1 of its
      W chunks straight to their owners, so all 7 xGMI links of a rank carry traffic at
-     once (a ring reduce-scatter would serialise on one link per step);
+     once (a ring reduce-scatter would serialise on one link per step).  By default steps
+     1-2 are pipelined instead: one partial kernel per destination chunk, each chunk sent
+     (pairwise send/recv, a shifted exchange) while the next one computes;
   3. combine kernel on the received [W][B*H][L/W][d] = the W partials of rank r's query
      rows -> O rows [r*L/W, (r+1)*L/W) of every head;
   4. optionally all_gather to a replicated O.
@@ -33,6 +35,12 @@ def _combine_fn(o_part, lse, B, H, dtype):
     return ops.combine(o_part, lse, B, H, dtype)
 
 
+def _partial_chunk_fn(q_rows, k, v, o_out, lse_out, partial_dtype):
+    """Partials of one chunk of query rows: q_rows a [B, H, Lc, d] row range of q (a view,
+    addressed in place), results into o_out [B*H, Lc, d] and lse_out [B*H, Lc]."""
+    ops.attention_partial(q_rows, k, v, partial_dtype=partial_dtype, o_part=o_out[None], lse=lse_out[None])
+
+
 def shard_bounds(L, world, rank):
     """Key range [lo, hi) of rank's shard (equal shards; L % world == 0)."""
     if L % world:
@@ -41,19 +49,65 @@ def shard_bounds(L, world, rank):
     return rank * n, (rank + 1) * n
 
 
+def _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc):
+    """Steps 1-2 pipelined: the partials are computed one destination chunk at a time, and
+    chunk j is handed to RCCL (send to rank j, matched receive from the rank sending to us)
+    as soon as its kernel is queued, so its transfer overlaps the next chunk's kernel.  Step s
+    pairs rank r -> r+s with r-s -> r (a shifted exchange: every step a perfect matching, all
+    ranks' links busy at once); the own chunk is computed last, straight into the receive
+    buffer.  RCCL waits on the compute stream at each send; the compute stream never waits
+    for RCCL until the combine."""
+    B, H, _, d = q.shape
+    rank = dist.get_rank(group)
+    lse_dtype = torch.float64 if q.dtype == torch.float64 else torch.float32
+    o_send = torch.empty((world, B * H, Lc, d), dtype=partial_dtype, device=q.device)
+    lse_send = torch.empty((world, B * H, Lc), dtype=lse_dtype, device=q.device)
+    o_recv, lse_recv = torch.empty_like(o_send), torch.empty_like(lse_send)
+
+    def peer(r):
+        return dist.get_global_rank(group, r) if group is not None else r
+
+    works = []
+    for s in range(1, world):
+        dst, src = (rank + s) % world, (rank - s) % world
+        _partial_chunk_fn(q[:, :, dst * Lc:(dst + 1) * Lc], k_shard, v_shard, o_send[dst], lse_send[dst],
+                          partial_dtype)
+        works += dist.batch_isend_irecv([
+            dist.P2POp(dist.isend, o_send[dst], peer(dst), group),
+            dist.P2POp(dist.irecv, o_recv[src], peer(src), group),
+            dist.P2POp(dist.isend, lse_send[dst], peer(dst), group),
+            dist.P2POp(dist.irecv, lse_recv[src], peer(src), group),
+        ])
+    _partial_chunk_fn(q[:, :, rank * Lc:(rank + 1) * Lc], k_shard, v_shard, o_recv[rank], lse_recv[rank],
+                      partial_dtype)
+    for w in works:
+        w.wait()
+    return o_recv, lse_recv
+
+
 def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=torch.bfloat16,
-                      gather=False):
+                      gather=False, overlap=True):
     """Sharded split-KV forward.
 
     q: [B, H, L, d] (identical on every rank); k_shard / v_shard: this rank's keys
     [B, H, L/W, d].  Returns this rank's query rows [B, H, L/W, d] of O, or the full
-    [B, H, L, d] O when ``gather``.
+    [B, H, L, d] O when ``gather``.  ``overlap`` (W > 1): per-destination partial kernels
+    pipelined with pairwise send/recv (_exchange_overlapped); otherwise one partial kernel
+    over all rows, then all_to_all_single.
     """
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     B, H, L, d = q.shape
     if L % world:
         raise ValueError(f"L={L} must be divisible by world size {world}")
     Lc = L // world
+    if world > 1 and overlap:
+        o_recv, lse_recv = _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc)
+        o_local = _combine_fn(o_recv, lse_recv, B, H, q.dtype)
+        if not gather:
+            return o_local
+        parts = [torch.empty_like(o_local) for _ in range(world)]
+        dist.all_gather(parts, o_local.contiguous(), group=group)
+        return torch.cat(parts, dim=2)
     o_part, lse = _partial_fn(q, k_shard, v_shard, Lc, partial_dtype)  # [W, BH, Lc, d], [W, BH, Lc]
     if world > 1:
         o_recv = torch.empty_like(o_part)

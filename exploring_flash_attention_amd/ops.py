@@ -278,7 +278,16 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None,
     log-sum-exp (of the scores times log2(e)/sqrt(d)); fp32 partials and lse by default,
     fp64 for fp64 inputs.
     """
-    _check_qkv(q, k, v, same_len=False)
+    _check_qkv(q, k, v, same_len=False, strided=True)
+    if not (k.is_contiguous() and v.is_contiguous()):
+        k, v = k.contiguous(), v.contiguous()
+    qst = None
+    if not q.is_contiguous():  # a row range of a longer q (the multi-GPU chunks): in place
+        st = _stride_args(q, k, v, q)
+        if st is False:
+            q = q.contiguous()
+        else:
+            qst = st[0]
     B, H, Lq, d = q.shape
     Lk = k.shape[2]
     cr = Lq if chunk_rows is None else int(chunk_rows)
@@ -289,8 +298,12 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None,
     lse_dtype = torch.float64 if q.dtype == torch.float64 else torch.float32
     o_part = _out(o_part, q, (nch, B * H, cr, d), partial_dtype)
     lse = _out(lse, q, (nch, B * H, cr), lse_dtype)
-    check(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
-                               cr, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
+    if qst is None:
+        check(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
+                                   cr, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
+    else:
+        check(lib().fa_fwd_partial_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
+                                      cr, qst, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
     return o_part, lse
 
 

@@ -175,6 +175,16 @@ int fa_fwd_partial(const void* q, const void* k, const void* v,
                    int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d,
                    int64_t chunk_rows, int dtype, int partial_dtype, void* stream);
 
+/* fa_fwd_partial with a strided q: q_strides = {batch, head, row} element strides of the
+ * [B, H, Lq, d] query view (NULL = contiguous), e.g. rows [c*Lq, (c+1)*Lq) of a longer
+ * [B, H, L, d] tensor -- the multi-GPU path computes one destination rank's chunk of the
+ * partials per launch this way, so the exchange of one chunk overlaps the next one's
+ * compute.  k, v contiguous; bf16 / fp16 only when strided. */
+int fa_fwd_partial_ex(const void* q, const void* k, const void* v,
+                      void* o_part, void* lse,
+                      int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d,
+                      int64_t chunk_rows, const int64_t* q_strides,
+                      int dtype, int partial_dtype, void* stream);
 /* Combine num_splits partials: o_part [num_splits][B*H][L][d] (partial_dtype),
  * lse [num_splits][B*H][L] (fp32, base 2; fp64 for FA_DTYPE_FP64) -> o [B, H, L, d] (dtype), using
  * O = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M), M = max_s lse_s

@@ -41,21 +41,30 @@ def _oracle_combine(o_part, lse, B, H, dtype):
     return torch.from_numpy(O.reshape(B, H, L, d)).to(dtype)
 
 
-def _worker(rank, world, port, result_path):
+def _oracle_partial_chunk(q_rows, k, v, o_out, lse_out, partial_dtype):
+    """The chunked partial of the overlapped path: same layouts as the kernel writes."""
+    assert not q_rows.is_contiguous() or q_rows.shape[2] == q_rows.stride(1) // q_rows.shape[3]
+    o, lse = _oracle_partial(q_rows.contiguous(), k, v, q_rows.shape[2], partial_dtype)
+    o_out.copy_(o[0])
+    lse_out.copy_(lse[0].to(lse_out.dtype))
+
+
+def _worker(rank, world, port, result_path, overlap):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from exploring_flash_attention_amd import dist as fdist
     fdist._partial_fn = _oracle_partial
     fdist._combine_fn = _oracle_combine
+    fdist._partial_chunk_fn = _oracle_partial_chunk
     g = torch.Generator().manual_seed(0)
     B, H, L, d = 2, 3, 64, 32
     q, k, v = (torch.randn(B, H, L, d, generator=g, dtype=torch.float64) for _ in range(3))
     lo, hi = fdist.shard_bounds(L, world, rank)
     local = fdist.splitkv_attention(q, k[:, :, lo:hi].contiguous(), v[:, :, lo:hi].contiguous(),
-                                    partial_dtype=torch.float64)
+                                    partial_dtype=torch.float64, overlap=overlap)
     full = fdist.splitkv_attention(q, k[:, :, lo:hi].contiguous(), v[:, :, lo:hi].contiguous(),
-                                   partial_dtype=torch.float64, gather=True)
+                                   partial_dtype=torch.float64, gather=True, overlap=overlap)
     ref = attention_fp64(q.numpy(), k.numpy(), v.numpy())
     err_local = np.abs(local.numpy() - ref[:, :, lo:hi]).max()
     err_full = np.abs(full.numpy() - ref).max()
@@ -64,11 +73,13 @@ def _worker(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("overlap", [False, True], ids=["all_to_all", "overlapped"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_splitkv_exchange_gloo(tmp_path, world):
+def test_splitkv_exchange_gloo(tmp_path, world, overlap):
     port = _free_port()
     path = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, port, path), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, path, overlap), nprocs=world, join=True,
+                       start_method="spawn")
     for r in range(world):
         err_local, err_full, *_ = open(f"{path}.{r}").read().split(" ", 2)
         assert float(err_local) < 1e-6 and float(err_full) < 1e-6  # fp32 lse, as on the GPU

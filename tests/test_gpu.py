@@ -447,6 +447,25 @@ def test_dist_single_rank_path_on_gpu(gpu):
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("pdtype", [torch.bfloat16, torch.float32], ids=["pbf16", "p32"])
+def test_dist_chunked_partials_match(gpu, pdtype):
+    """The overlapped multi-GPU path computes the partials one destination chunk at a time
+    from row-range views of q (fa_fwd_partial_ex, strided q): bitwise equal to the one-launch
+    partial kernel's all-to-all send layout, for W = 4 chunks (incl. a tail chunk length)."""
+    from exploring_flash_attention_amd import dist as fdist
+    from exploring_flash_attention_amd import ops
+    for (B, H, L, Lk, d) in ((2, 3, 512, 130, 128), (1, 2, 4 * 72, 64, 64)):
+        q, k, v = (x.to(gpu) for x in _inputs(B, H, L, d, torch.bfloat16, seed=41, Lk=Lk))
+        W, Lc = 4, L // 4
+        o_ref, lse_ref = ops.attention_partial(q, k, v, chunk_rows=Lc, partial_dtype=pdtype)
+        o_send = torch.empty_like(o_ref)
+        lse_send = torch.empty_like(lse_ref)
+        for j in range(W):
+            fdist._partial_chunk_fn(q[:, :, j * Lc:(j + 1) * Lc], k, v, o_send[j], lse_send[j], pdtype)
+        torch.cuda.synchronize()
+        assert torch.equal(o_send, o_ref) and torch.equal(lse_send, lse_ref)
+
+
 def test_dist_native_rccl_single_rank(gpu):
     """fa_fwd_v2_dist (C ABI, RCCL communicator of libfa_mi355x_dist.so) at world size 1:
     partial -> (no exchange) -> combine, rows and gathered forms, bf16 and fp64."""
