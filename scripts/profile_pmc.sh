@@ -13,7 +13,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_
              "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
              "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $group -d $OUT/p$i -o run --output-format csv -- \
+  timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $group -d $OUT/p$i -o run --output-format csv -- \
      python scripts/run_kernel.py $CFG 5 > $OUT/p$i.log 2>&1; rc=$?
   echo "pass $i ($group) rc=$rc"
   case $rc in 0) ;; *) tail -5 $OUT/p$i.log; exit $rc ;; esac
