@@ -37,9 +37,6 @@
 // Build knobs for A/B experiments (scripts/build_variants.sh, scripts/ab.py); the
 // defaults are the measured-best settings.  FA_ABL_* are ablations (wrong results,
 // timing only) used to attribute time to the kernel's phases.
-#ifndef FA_QK_SCHED
-#define FA_QK_SCHED 0
-#endif
 #ifndef FA_WIDE_STORE
 #define FA_WIDE_STORE 1
 #endif
@@ -55,8 +52,17 @@
 #ifndef FA_PRIO
 #define FA_PRIO 0
 #endif
+// a sched_barrier between the P.V MFMAs and the next tile's mask + row max, per head dim
+// (bitmask as FA_UNIFORM_WID): after the v_maximum3 change it costs C3 0.7-1.2 %, C4 1-1.6 %
+// (without it hipcc interleaves the row max with the last P.V MFMAs), C2 / d=64 0, and still
+// pays 1.7 % at d=256
 #ifndef FA_ROWMAX_FENCE
-#define FA_ROWMAX_FENCE 1
+#define FA_ROWMAX_FENCE 0x8
+#endif
+// FA_SGB: explicit sched_group_barrier pattern for the steady step (1: QK phase 16 x {MFMA,
+// 1 LDS read, 5 VALU}, PV phase 16 x {MFMA, 2 LDS reads, 3 VALU}; 2: 4 / 4 VALU)
+#ifndef FA_SGB
+#define FA_SGB 0
 #endif
 #ifndef FA_ABL_NODMAWAIT
 #define FA_ABL_NODMAWAIT 0
@@ -94,9 +100,6 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 // packed fp32 softmax arithmetic for d <= FA_PK_MAXD (0 = off)
 #ifndef FA_PK_MAXD
 #define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
-#endif
-#ifndef FA_QK_LEAD
-#define FA_QK_LEAD 4
 #endif
 
 // FA_STAMPS (diagnostic builds only): wave 0 of every workgroup writes s_memtime stamps at
@@ -513,12 +516,25 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             }
         });
         if constexpr (MORE) {
-#if FA_ROWMAX_FENCE
-            __builtin_amdgcn_sched_barrier(0);
-#endif
+            if constexpr ((FA_ROWMAX_FENCE & d_bit(D)) != 0) __builtin_amdgcn_sched_barrier(0);
             if constexpr (MASKNEXT) mask(t + 1, sn);
             rowmax(sn, mx);
         }
+#if FA_SGB
+        if constexpr (MORE && NKB * NDB * 2 == 16 && NKB * NKS == 16) {
+            constexpr int VQ = FA_SGB == 1 ? 5 : 4, VP = FA_SGB == 1 ? 3 : 4;
+            static_for<16>([&](auto) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, VQ, 0);
+            });
+            static_for<16>([&](auto) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, VP, 0);
+            });
+        }
+#endif
 #if FA_ABL_NODMAWAIT
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
