@@ -21,6 +21,7 @@ FA_DTYPE_FP16 = 0
 FA_DTYPE_BF16 = 1
 FA_DTYPE_FP32 = 2
 FA_DTYPE_FP64 = 3
+FA_DTYPE_FP16_SCALED = 4  # split-KV partials: fp16 scaled per row by a power of two
 
 FA_KV_TILES_AUTO = -1  # kv_tiles_per_block: split chosen from the device's occupancy
 

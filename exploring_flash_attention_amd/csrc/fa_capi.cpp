@@ -49,9 +49,10 @@ int check_partial_dtype(int pdtype, int dtype, fa::Elem* e) {
         return fail(FA_ERR_UNSUPPORTED, "fp64 inputs take fp64 partials (got partial dtype %d)", pdtype);
     }
     if (pdtype == FA_DTYPE_FP32) { *e = fa::Elem::F32; return FA_OK; }
+    if (pdtype == FA_DTYPE_FP16_SCALED) { *e = fa::Elem::F16S; return FA_OK; }
     if (pdtype == dtype) return check_dtype(dtype, e);
-    return fail(FA_ERR_UNSUPPORTED, "partial dtype %d must be FA_DTYPE_FP32 or the input dtype %d",
-                pdtype, dtype);
+    return fail(FA_ERR_UNSUPPORTED,
+                "partial dtype %d must be FA_DTYPE_FP32, FA_DTYPE_FP16_SCALED or the input dtype %d", pdtype, dtype);
 }
 
 int check_shape(int64_t B, int64_t H, int64_t L, int64_t d) {
@@ -162,7 +163,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // lse [S][BH][nqt][BQ] (fp32), both in the kernel's fragment order, then one uint32
 // counter per (b*h, query tile).  Every part 256-byte aligned.
 struct V2Layout {
-    size_t o_bytes, lse_off, cnt_off, total;
+    size_t o_bytes, lse_off, esc_off, cnt_off, total;
     int64_t ngroups;
 };
 V2Layout v2_layout(int64_t BH, int64_t L, int64_t d, int ns, fa::Elem pe) {
@@ -181,7 +182,8 @@ V2Layout v2_layout(int64_t BH, int64_t L, int64_t d, int ns, fa::Elem pe) {
     w.ngroups = BH * nqt;
     w.o_bytes = align256(rows * d * esz);
     w.lse_off = w.o_bytes;
-    w.cnt_off = w.lse_off + align256(rows * sizeof(float));
+    w.esc_off = w.lse_off + align256(rows * sizeof(float));
+    w.cnt_off = w.esc_off + (pe == fa::Elem::F16S ? align256(rows * sizeof(float)) : 0);
     w.total = w.cnt_off + align256((size_t)w.ngroups * sizeof(unsigned));
     return w;
 }
@@ -378,6 +380,7 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     }
     a.o = workspace;
     a.lse = (float*)((char*)workspace + w.lse_off);
+    a.esc = (float*)((char*)workspace + w.esc_off);
     a.counters = (unsigned*)((char*)workspace + w.cnt_off);
     a.o_final = o;
     // the kernel leaves every counter at zero; clearing them here makes a call that follows
@@ -408,6 +411,7 @@ int fa_fwd_partial_ex(const void* q, const void* k, const void* v, void* o_part,
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (int st = check_ptrs(q, k, v, o_part)) return st;
     if (!lse) return fail(FA_ERR_INVALID_ARG, "lse is NULL");
+    if (pe == fa::Elem::F16S) return fail(FA_ERR_UNSUPPORTED, "FA_DTYPE_FP16_SCALED partials: fa_fwd_v2 only");
     if (chunk_rows <= 0 || Lq % chunk_rows)
         return fail(FA_ERR_INVALID_ARG, "chunk_rows=%lld must divide Lq=%lld", (long long)chunk_rows,
                     (long long)Lq);
@@ -431,6 +435,7 @@ int fa_combine(const void* o_part, const void* lse, void* o, int64_t num_splits,
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (!o_part || !lse || !o) return fail(FA_ERR_INVALID_ARG, "null pointer");
+    if (pe == fa::Elem::F16S) return fail(FA_ERR_UNSUPPORTED, "FA_DTYPE_FP16_SCALED partials: fa_fwd_v2 only");
     if (num_splits <= 0 || num_splits > 65536)
         return fail(FA_ERR_INVALID_ARG, "num_splits=%lld out of range", (long long)num_splits);
     fa::CombineArgs c{};

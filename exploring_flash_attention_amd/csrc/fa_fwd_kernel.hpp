@@ -32,6 +32,8 @@
 //   * blockIdx is remapped so that all query tiles of one (b,h) land on one XCD and
 //     share that head's K/V in the XCD's L2.
 #pragma once
+#include <type_traits>
+
 #include "fa_device.hpp"
 
 // Build knobs for A/B experiments (scripts/build_variants.sh, scripts/ab.py); the
@@ -652,7 +654,10 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         };
         const int lse_off = (wid * RB) * 32 * 4 + l32 * 4;  // + r*128
 
-        float inv[RB], lse_own[RB];
+        constexpr bool SCALED = std::is_same_v<PT, f16s_t>;  // fp16 partials, per-row 2^-e
+        using PH = std::conditional_t<SCALED, _Float16, T>;   // 16-bit partial element type
+        auto e_rsrc = [&](int sp) { return make_rsrc(a.esc + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
+        float inv[RB], lse_own[RB], esc_own[RB];
         {
             const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
 #pragma unroll
@@ -660,6 +665,18 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                 const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
                 inv[r] = 1.f / l_tot;
                 lse_own[r] = m[r] + __builtin_amdgcn_logf(l_tot);
+                esc_own[r] = 0.f;
+                if constexpr (SCALED) {
+                    // the row's largest |O / l| below 1 after the exact scale 2^-e
+                    float mx = 0.f;
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) mx = fmax_nc(mx, __builtin_fabsf(o[r][db][i]));
+                    const int e = __builtin_amdgcn_frexp_expf(pair_max(mx) * inv[r]);
+                    esc_own[r] = (float)e;
+                    inv[r] = __builtin_amdgcn_ldexpf(inv[r], -e);
+                }
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
                     const int db = f >> 2, g4 = f & 3;
@@ -670,13 +687,17 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                                          __float_as_uint(src[2] * inv[r]), __float_as_uint(src[3] * inv[r])};
                         __builtin_amdgcn_raw_buffer_store_b128(u, ors, frag_off(r, f), 0, SC1);
                     } else {
-                        const u32x2 u = {pack2<T>(src[0] * inv[r], src[1] * inv[r]),
-                                         pack2<T>(src[2] * inv[r], src[3] * inv[r])};
+                        const u32x2 u = {pack2<PH>(src[0] * inv[r], src[1] * inv[r]),
+                                         pack2<PH>(src[2] * inv[r], src[3] * inv[r])};
                         __builtin_amdgcn_raw_buffer_store_b64(u, ors, frag_off(r, f), 0, SC1);
                     }
                 }
-                if (hf == 0)
+                if (hf == 0) {
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse_own[r]), lrs, lse_off + r * 128, 0, SC1);
+                    if constexpr (SCALED)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(esc_own[r]), e_rsrc(split),
+                                                              lse_off + r * 128, 0, SC1);
+                }
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -715,8 +736,15 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             } else {
                 const unsigned w = u[j >> 1];
                 const unsigned short h = (unsigned short)((j & 1) ? (w >> 16) : (w & 0xffff));
-                return (float)__builtin_bit_cast(T, h);
+                return (float)__builtin_bit_cast(PH, h);
             }
+        };
+        // weight of split sp's stored values: 2^(lse - M), times 2^e for scaled partials
+        auto load_esc = [&](int sp, int r) {
+            if constexpr (SCALED)
+                return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off + r * 128, 0, SC1));
+            else
+                return 0.f;
         };
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
@@ -726,31 +754,35 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             f32x16 acc[NDB];
 #pragma unroll
             for (int db = 0; db < NDB; ++db) acc[db] = f32x16{};
-            auto fma_split = [&](const frag_t (&fr)[NF], float w) {
+            auto fma_split = [&](const frag_t (&fr)[NF], float w, float es) {
+                const float wv = SCALED ? __builtin_amdgcn_ldexpf(w, (int)es) : w;
 #pragma unroll
                 for (int f = 0; f < NF; ++f)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        acc[f >> 2][4 * (f & 3) + j] = __builtin_fmaf(w, unpack(fr[f], j), acc[f >> 2][4 * (f & 3) + j]);
+                        acc[f >> 2][4 * (f & 3) + j] = __builtin_fmaf(wv, unpack(fr[f], j), acc[f >> 2][4 * (f & 3) + j]);
                 wsum += w;
             };
             // two splits in flight: the loads of split sp+1 overlap the FMAs of split sp
             frag_t fa_[NF], fb_[NF];
-            float wa, wb = 0.f;
+            float wa, wb = 0.f, ea, eb = 0.f;
             load_frags(0, r, fa_);
             wa = __builtin_amdgcn_exp2f(load_lse(0, r) - M);
+            ea = load_esc(0, r);
             for (int sp = 0; sp < ns; sp += 2) {
                 if (sp + 1 < ns) {
                     load_frags(sp + 1, r, fb_);
                     wb = __builtin_amdgcn_exp2f(load_lse(sp + 1, r) - M);
+                    eb = load_esc(sp + 1, r);
                 }
-                fma_split(fa_, wa);
+                fma_split(fa_, wa, ea);
                 if (sp + 1 < ns) {
                     if (sp + 2 < ns) {
                         load_frags(sp + 2, r, fa_);
                         wa = __builtin_amdgcn_exp2f(load_lse(sp + 2, r) - M);
+                        ea = load_esc(sp + 2, r);
                     }
-                    fma_split(fb_, wb);
+                    fma_split(fb_, wb, eb);
                 }
             }
             const int64_t q_row = q_row0 + 32 * r;

@@ -46,7 +46,13 @@ constexpr int kWavesPerSimd = kRB == 1 ? 2 : 1;  // occupancy the register budge
 // d = 256 holds 64 Q and 128 O registers per lane: one wave per SIMD, AGPRs in use
 constexpr int waves_per_simd(int d) { return d > 128 ? 1 : kWavesPerSimd; }
 
-enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2, F64 = 3 };
+enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2, F64 = 3, F16S = 4 };
+// F16S (split-KV partials only): fp16 values scaled per row by a power of two 2^-e so that the
+// row's largest |value| is below 1, e stored beside the lse -- half the bytes of fp32 with
+// 11 significant bits relative to the row maximum and no fp16 range limit
+struct f16s_t {
+    _Float16 x;
+};
 
 // Arguments of the forward kernel (final and partial modes share one struct).
 struct FwdArgs {
@@ -67,6 +73,7 @@ struct FwdArgs {
     // fused split mode only: the last workgroup of each (query tile, b*h) to finish combines
     // the splits (see fa_fwd.hip); o / lse then hold the workspace in fragment order
     unsigned* counters;      // [BH][nqt], zero before the launch; left zero after it
+    float* esc;              // F16S partials: per-row scale exponents, laid out as lse
     void* o_final;           // [BH][Lq][D] (T)
     // fp64 mode (fa_fwd64.hip)
     double scale_log2_64;    // log2(e) / sqrt(d) in double

@@ -63,6 +63,11 @@ typedef enum fa_dtype {
     FA_DTYPE_FP16 = 0,       /* IEEE binary16 storage, fp32 accumulate */
     FA_DTYPE_BF16 = 1,       /* bfloat16 storage, fp32 accumulate */
     FA_DTYPE_FP32 = 2,       /* only valid as the split-KV partial-output type */
+    FA_DTYPE_FP16_SCALED = 4, /* only as fa_fwd_v2's partial-output type: fp16 partials
+                                 scaled per row by a power of two (the row's largest |value|
+                                 below 1), the exponent kept beside the lse -- half the
+                                 workspace traffic of FA_DTYPE_FP32, 11 significant bits
+                                 relative to each row's maximum, no fp16 range limit */
     FA_DTYPE_FP64 = 3        /* IEEE binary64 throughout (the reference's USE_FP64 build,
                                 flash_attention_v1/CUDA/flash_attention_v1.h:29-41): fp64
                                 MFMA, fp64 softmax, fp64 partials and lse */
@@ -131,7 +136,7 @@ int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o,
 
 /* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split is
  * kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
- * FA_DTYPE_FP32 or the input dtype.  *num_splits (may be NULL) receives the split count. */
+ * FA_DTYPE_FP32, the input dtype or FA_DTYPE_FP16_SCALED.  *num_splits (may be NULL) receives the split count. */
 int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d,
                              int kv_tiles_per_block, int dtype, int partial_dtype,
                              size_t* bytes, int* num_splits);

@@ -157,13 +157,14 @@ def _variants():
         "tiled_d": lambda q, k, v: ops.attention_tiled_d(q, k, v, 16, 32),
         "v2_kvtpb1_f32": lambda q, k, v: ops.attention_v2(q, k, v, 1, partial_dtype=torch.float32),
         "v2_kvtpb4_p16": lambda q, k, v: ops.attention_v2(q, k, v, 4, partial_dtype=q.dtype),
+        "v2_kvtpb1_f16s": lambda q, k, v: ops.attention_v2(q, k, v, 1, partial_dtype=ops.PARTIAL_FP16_SCALED),
     }
 
 
 SHAPES = [(1, 1, 1), (1, 2, 65), (2, 3, 200), (1, 2, 512)]
 
 
-@pytest.mark.parametrize("variant", ["v1", "tiled_d", "v2_kvtpb1_f32", "v2_kvtpb4_p16"])
+@pytest.mark.parametrize("variant", ["v1", "tiled_d", "v2_kvtpb1_f32", "v2_kvtpb4_p16", "v2_kvtpb1_f16s"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
 @pytest.mark.parametrize("d", [32, 64, 128, 256])
 def test_matrix(gpu, variant, dtype, d):
@@ -255,6 +256,33 @@ def test_empty_inputs(gpu):
     O = v1.flash_attention_tiled(Z, Z, Z)
     assert O.shape == (0, 32) and O.dtype == np.float64
     assert fa.flash_attention_v1(Z, Z, Z).shape == (0, 32)
+
+
+def test_scaled_fp16_partials(gpu):
+    """FA_DTYPE_FP16_SCALED split-KV partials: as accurate as fp32 partials to well within the
+    output's own bf16 rounding, bitwise repeatable, and free of fp16's range limit (|V| up to
+    1e6, where plain fp16 partials would overflow)."""
+    from exploring_flash_attention_amd import ops
+    S = ops.PARTIAL_FP16_SCALED
+    for (B, H, L, d, scale) in ((2, 3, 700, 128, 1.0), (1, 2, 1024, 64, 1e6), (1, 1, 333, 32, 1e-4)):
+        q, k, v = _inputs(B, H, L, d, torch.bfloat16, seed=50)
+        v = (v.float() * scale).to(torch.bfloat16)
+        ref = _ref(q, k, v)
+        qd, kd, vd = q.to(gpu), k.to(gpu), v.to(gpu)
+        for kvt in (1, 2):
+            o32 = ops.attention_v2(qd, kd, vd, kvt, partial_dtype=torch.float32).float().cpu().numpy()
+            o16 = ops.attention_v2(qd, kd, vd, kvt, partial_dtype=S)
+            o16b = ops.attention_v2(qd, kd, vd, kvt, partial_dtype=S)
+            torch.cuda.synchronize()
+            assert torch.equal(o16, o16b)
+            o16 = o16.float().cpu().numpy()
+            assert np.isfinite(o16).all()
+            amax = np.abs(ref).max()
+            # 2^-11 relative to each row's largest |partial| per split, against bf16 output
+            # rounding of 2^-9 relative: the two paths differ by at most a few output ulps
+            assert np.abs(o16 - o32).max() <= 1.5e-2 * amax, (L, d, scale, kvt)
+            e32, e16 = np.abs(o32 - ref).max(), np.abs(o16 - ref).max()
+            assert e16 <= 1.25 * e32 + 1e-3 * amax, (e16, e32)
 
 
 def test_golden_flat_surface_d16(gpu):
