@@ -351,8 +351,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w64_kernel(FwdArgs a) {
             for (int b2 = 0; b2 < 2; ++b2)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
-                    if (b2 > 0 || i >= 4) m4[i & 3] = fmaxf(m4[i & 3], s[rb][b2][i]);
-            mx[rb] = pair_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]))) * c;
+                    if (b2 > 0 || i >= 4) m4[i & 3] = fmax_nc(m4[i & 3], s[rb][b2][i]);
+            mx[rb] = pair_max(fmax_nc(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]))) * c;
         }
     };
     // O block rows of row block RB *= alpha (rare: defer-max)
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w64_kernel(FwdArgs a) {
                 static_for<4>([&](auto j_c) {
                     constexpr int J = decltype(j_c)::value;
                     if constexpr (MB == 0 && I0 == 0) m4[R][J] = sn[R][0][J];
-                    else m4[R][J] = fmaxf(m4[R][J], sn[R][MB][I0 + J]);
+                    else m4[R][J] = fmax_nc(m4[R][J], sn[R][MB][I0 + J]);
                 });
             }
             if constexpr (PP % 4 == 3 && FR + 1 < 8) lds_wait(vbuf[(FR + 1) & 1]);
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w64_kernel(FwdArgs a) {
         if constexpr (MORE) {
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb)
-                mx[rb] = pair_max(fmaxf(fmaxf(m4[rb][0], m4[rb][1]), fmaxf(m4[rb][2], m4[rb][3]))) * c;
+                mx[rb] = pair_max(fmax_nc(fmax_nc(m4[rb][0], m4[rb][1]), fmax_nc(m4[rb][2], m4[rb][3]))) * c;
         }
         __syncthreads();  // drains the DMA (vmcnt(0)): K(t+2), V(t+1) landed
     };
