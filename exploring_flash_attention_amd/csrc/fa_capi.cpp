@@ -411,7 +411,6 @@ int fa_fwd_partial_ex(const void* q, const void* k, const void* v, void* o_part,
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (int st = check_ptrs(q, k, v, o_part)) return st;
     if (!lse) return fail(FA_ERR_INVALID_ARG, "lse is NULL");
-    if (pe == fa::Elem::F16S) return fail(FA_ERR_UNSUPPORTED, "FA_DTYPE_FP16_SCALED partials: fa_fwd_v2 only");
     if (chunk_rows <= 0 || Lq % chunk_rows)
         return fail(FA_ERR_INVALID_ARG, "chunk_rows=%lld must divide Lq=%lld", (long long)chunk_rows,
                     (long long)Lq);
@@ -435,7 +434,6 @@ int fa_combine(const void* o_part, const void* lse, void* o, int64_t num_splits,
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (!o_part || !lse || !o) return fail(FA_ERR_INVALID_ARG, "null pointer");
-    if (pe == fa::Elem::F16S) return fail(FA_ERR_UNSUPPORTED, "FA_DTYPE_FP16_SCALED partials: fa_fwd_v2 only");
     if (num_splits <= 0 || num_splits > 65536)
         return fail(FA_ERR_INVALID_ARG, "num_splits=%lld out of range", (long long)num_splits);
     fa::CombineArgs c{};

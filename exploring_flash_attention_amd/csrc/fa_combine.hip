@@ -28,19 +28,24 @@ __device__ __forceinline__ unsigned short from_f(float f) {
 template <typename T, typename PT, int D>
 __global__ __launch_bounds__(256) void fa_combine_kernel(CombineArgs a) {
     constexpr int TPR = D / 8;  // threads per row
+    using PH = std::conditional_t<std::is_same_v<PT, f16s_t>, _Float16, T>;  // 16-bit element
     const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t row = gid / TPR;
     const int c8 = (int)(gid % TPR) * 8;
     if (row >= a.rows) return;
 
+    // scaled fp16 partials: {lse, e} per row, values stored as O/l * 2^-e
+    constexpr bool SCALED = std::is_same_v<PT, f16s_t>;
+    constexpr int LS = SCALED ? 2 : 1;
     float mx = -INFINITY;
-    for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, a.lse[s * a.rows + row]);
+    for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, a.lse[LS * (s * a.rows + row)]);
 
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float wsum = 0.f;
     for (int s = 0; s < a.nsplit; ++s) {
-        const float wgt = __builtin_amdgcn_exp2f(a.lse[s * a.rows + row] - mx);
+        float wgt = __builtin_amdgcn_exp2f(a.lse[LS * (s * a.rows + row)] - mx);
         wsum += wgt;
+        if constexpr (SCALED) wgt = __builtin_amdgcn_ldexpf(wgt, (int)a.lse[2 * (s * a.rows + row) + 1]);
         const int64_t base = ((int64_t)s * a.rows + row) * D + c8;
         if constexpr (sizeof(PT) == 4) {
             const f32x4 x0 = *(const f32x4*)((const float*)a.o_part + base);
@@ -54,8 +59,8 @@ __global__ __launch_bounds__(256) void fa_combine_kernel(CombineArgs a) {
             const u32x4 x = *(const u32x4*)((const unsigned short*)a.o_part + base);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                acc[2 * j] += wgt * to_f<T>((unsigned short)(x[j] & 0xffff));
-                acc[2 * j + 1] += wgt * to_f<T>((unsigned short)(x[j] >> 16));
+                acc[2 * j] += wgt * to_f<PH>((unsigned short)(x[j] & 0xffff));
+                acc[2 * j + 1] += wgt * to_f<PH>((unsigned short)(x[j] >> 16));
             }
         }
     }
@@ -87,6 +92,8 @@ hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStrea
     if (t == Elem::BF16 && pt == Elem::F32) return launch_c<__bf16, float>(d, a, s);
     if (t == Elem::F16 && pt == Elem::F16) return launch_c<_Float16, _Float16>(d, a, s);
     if (t == Elem::F16 && pt == Elem::F32) return launch_c<_Float16, float>(d, a, s);
+    if (t == Elem::BF16 && pt == Elem::F16S) return launch_c<__bf16, f16s_t>(d, a, s);
+    if (t == Elem::F16 && pt == Elem::F16S) return launch_c<_Float16, f16s_t>(d, a, s);
     return hipErrorInvalidValue;
 }
 

@@ -794,7 +794,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     for (int r = 0; r < RB; ++r) {
         const int64_t q_row = q_row0 + 32 * r;
         const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
-        const float inv = 1.f / l_tot;
+        float inv = 1.f / l_tot;
         if (q_row >= a.Lq) continue;
         if constexpr (MODE == kFinal) {
             store_row((unsigned short*)a.o + o_head + q_row * orow, o[r], inv);
@@ -802,6 +802,21 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
             const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
             PT* Op = (PT*)a.o + split * a.split_stride + row_lin * D;
+            // per-row scaled fp16 (as in the fused split): O/l * 2^-e with the row's largest
+            // |O/l| just below 1; the lse buffer then holds {lse, e} per row
+            constexpr bool SCALED = std::is_same_v<PT, f16s_t>;
+            using PH = std::conditional_t<SCALED, _Float16, T>;
+            float esc = 0.f;
+            if constexpr (SCALED) {
+                float mx = 0.f;
+#pragma unroll
+                for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) mx = fmax_nc(mx, __builtin_fabsf(o[r][db][i]));
+                const int e = __builtin_amdgcn_frexp_expf(pair_max(mx) * inv);
+                esc = (float)e;
+                inv = __builtin_amdgcn_ldexpf(inv, -e);
+            }
 #pragma unroll
             for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -813,13 +828,19 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                         *(f32x4*)(Op + col) = f;
                     } else {
                         u32x2 u;
-                        u[0] = pack2<T>(o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv);
-                        u[1] = pack2<T>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
+                        u[0] = pack2<PH>(o[r][db][4 * g4 + 0] * inv, o[r][db][4 * g4 + 1] * inv);
+                        u[1] = pack2<PH>(o[r][db][4 * g4 + 2] * inv, o[r][db][4 * g4 + 3] * inv);
                         *(u32x2*)((unsigned short*)Op + col) = u;
                     }
                 }
             // lse in log2 units: m + log2(l)  (v_log_f32 is log2)
-            if (hf == 0) a.lse[split * a.BH * a.Lq + row_lin] = m[r] + __builtin_amdgcn_logf(l_tot);
+            const float lse = m[r] + __builtin_amdgcn_logf(l_tot);
+            if (hf == 0) {
+                if constexpr (SCALED)
+                    *(float2*)(a.lse + 2 * (split * a.BH * a.Lq + row_lin)) = make_float2(lse, esc);
+                else
+                    a.lse[split * a.BH * a.Lq + row_lin] = lse;
+            }
         }
     }
     }

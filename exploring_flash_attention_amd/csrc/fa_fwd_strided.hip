@@ -43,7 +43,7 @@ hipError_t launch_fwd_strided(Elem t, Elem pt, int d, Mode mode, const FwdArgs& 
         if (t == Elem::BF16 && pt == Elem::F32) return launch_strided_d<__bf16, float, M>(d, a, s);
         if (t == Elem::F16 && pt == Elem::F16) return launch_strided_d<_Float16, _Float16, M>(d, a, s);
         if (t == Elem::F16 && pt == Elem::F32) return launch_strided_d<_Float16, float, M>(d, a, s);
-        if constexpr (M == kFused) {  // per-row scaled fp16 partials: fused split mode only
+        {  // per-row scaled fp16 partials
             if (t == Elem::BF16 && pt == Elem::F16S) return launch_strided_d<__bf16, f16s_t, M>(d, a, s);
             if (t == Elem::F16 && pt == Elem::F16S) return launch_strided_d<_Float16, f16s_t, M>(d, a, s);
         }

@@ -37,7 +37,8 @@ def _combine_fn(o_part, lse, B, H, dtype):
 
 def _partial_chunk_fn(q_rows, k, v, o_out, lse_out, partial_dtype):
     """Partials of one chunk of query rows: q_rows a [B, H, Lc, d] row range of q (a view,
-    addressed in place), results into o_out [B*H, Lc, d] and lse_out [B*H, Lc]."""
+    addressed in place), results into o_out [B*H, Lc, d] and lse_out [B*H, Lc] ([B*H, Lc, 2]
+    for scaled partials)."""
     ops.attention_partial(q_rows, k, v, partial_dtype=partial_dtype, o_part=o_out[None], lse=lse_out[None])
 
 
@@ -60,8 +61,10 @@ def _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc):
     B, H, _, d = q.shape
     rank = dist.get_rank(group)
     lse_dtype = torch.float64 if q.dtype == torch.float64 else torch.float32
-    o_send = torch.empty((world, B * H, Lc, d), dtype=partial_dtype, device=q.device)
-    lse_send = torch.empty((world, B * H, Lc), dtype=lse_dtype, device=q.device)
+    scaled = partial_dtype == ops.PARTIAL_FP16_SCALED  # fp16 rows, {lse, exponent} per row
+    o_send = torch.empty((world, B * H, Lc, d), dtype=torch.float16 if scaled else partial_dtype,
+                         device=q.device)
+    lse_send = torch.empty((world, B * H, Lc) + ((2,) if scaled else ()), dtype=lse_dtype, device=q.device)
     o_recv, lse_recv = torch.empty_like(o_send), torch.empty_like(lse_send)
 
     def peer(r):
@@ -85,7 +88,7 @@ def _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc):
     return o_recv, lse_recv
 
 
-def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=torch.bfloat16,
+def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=None,
                       gather=False, overlap=True):
     """Sharded split-KV forward.
 
@@ -93,8 +96,12 @@ def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=torch.bfloa
     [B, H, L/W, d].  Returns this rank's query rows [B, H, L/W, d] of O, or the full
     [B, H, L, d] O when ``gather``.  ``overlap`` (W > 1): per-destination partial kernels
     pipelined with pairwise send/recv (_exchange_overlapped); otherwise one partial kernel
-    over all rows, then all_to_all_single.
+    over all rows, then all_to_all_single.  ``partial_dtype`` (the format sent over xGMI):
+    default per-row scaled fp16 (ops.PARTIAL_FP16_SCALED) -- the bytes of bf16 partials with
+    3 more significant bits; fp64 for fp64 inputs.
     """
+    if partial_dtype is None:
+        partial_dtype = torch.float64 if q.dtype == torch.float64 else ops.PARTIAL_FP16_SCALED
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     B, H, L, d = q.shape
     if L % world:

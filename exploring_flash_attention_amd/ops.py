@@ -286,7 +286,9 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None,
     Returns ``(o_part, lse)`` with o_part ``[Lq/chunk_rows, B*H, chunk_rows, d]`` holding the
     normalised partial output and lse ``[Lq/chunk_rows, B*H, chunk_rows]`` its base-2
     log-sum-exp (of the scores times log2(e)/sqrt(d)); fp32 partials and lse by default,
-    fp64 for fp64 inputs.
+    fp64 for fp64 inputs.  ``partial_dtype=PARTIAL_FP16_SCALED``: o_part is fp16 holding each
+    row times 2^-e (the row's largest |value| just below 1) and lse gains a trailing dim of 2,
+    ``{lse, e}`` per row -- ``combine`` recognises the format by that dim.
     """
     _check_qkv(q, k, v, same_len=False, strided=True)
     if not (k.is_contiguous() and v.is_contiguous()):
@@ -306,8 +308,9 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None,
     nch = Lq // cr
     partial_dtype = _default_pdtype(q.dtype, partial_dtype)
     lse_dtype = torch.float64 if q.dtype == torch.float64 else torch.float32
-    o_part = _out(o_part, q, (nch, B * H, cr, d), partial_dtype)
-    lse = _out(lse, q, (nch, B * H, cr), lse_dtype)
+    scaled = partial_dtype == PARTIAL_FP16_SCALED
+    o_part = _out(o_part, q, (nch, B * H, cr, d), torch.float16 if scaled else partial_dtype)
+    lse = _out(lse, q, (nch, B * H, cr, 2) if scaled else (nch, B * H, cr), lse_dtype)
     if qst is None:
         check(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
                                    cr, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
@@ -318,17 +321,24 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None,
 
 
 def combine(o_part, lse, B, H, dtype, out=None):
-    """Combine ``S`` partials o_part ``[S, B*H, L, d]`` / lse ``[S, B*H, L]`` -> ``[B, H, L, d]``."""
+    """Combine ``S`` partials o_part ``[S, B*H, L, d]`` / lse ``[S, B*H, L]`` -> ``[B, H, L, d]``.
+
+    An lse of shape ``[S, B*H, L, 2]`` marks fp16 per-row scaled partials (``attention_partial``
+    with ``PARTIAL_FP16_SCALED``)."""
     _check_tensor("o_part", o_part, ndim=4)
+    scaled = lse.dim() == 4
     _check_tensor("lse", lse, torch.float64 if o_part.dtype == torch.float64 else torch.float32,
-                  o_part.device, ndim=3)
+                  o_part.device, ndim=4 if scaled else 3)
     S, BH, L, d = o_part.shape
-    if BH != B * H or tuple(lse.shape) != (S, BH, L):
+    if BH != B * H or tuple(lse.shape) != ((S, BH, L, 2) if scaled else (S, BH, L)):
         raise ValueError(f"inconsistent shapes o_part {tuple(o_part.shape)} lse {tuple(lse.shape)} "
                          f"B={B} H={H}")
+    if scaled and o_part.dtype != torch.float16:
+        raise ValueError(f"scaled partials (lse [..., 2]) are fp16, got {o_part.dtype}")
     o = _out(out, o_part, (B, H, L, d), dtype)
+    pd = PARTIAL_FP16_SCALED if scaled else o_part.dtype
     check(lib().fa_combine(_ptr(o_part), _ptr(lse), _ptr(o), S, B, H, L, d, _DTYPES[dtype],
-                           _PDTYPES[o_part.dtype], _stream(o_part)))
+                           _PDTYPES[pd], _stream(o_part)))
     return o
 
 

@@ -63,11 +63,11 @@ typedef enum fa_dtype {
     FA_DTYPE_FP16 = 0,       /* IEEE binary16 storage, fp32 accumulate */
     FA_DTYPE_BF16 = 1,       /* bfloat16 storage, fp32 accumulate */
     FA_DTYPE_FP32 = 2,       /* only valid as the split-KV partial-output type */
-    FA_DTYPE_FP16_SCALED = 4, /* only as fa_fwd_v2's partial-output type: fp16 partials
-                                 scaled per row by a power of two (the row's largest |value|
-                                 below 1), the exponent kept beside the lse -- half the
-                                 workspace traffic of FA_DTYPE_FP32, 11 significant bits
-                                 relative to each row's maximum, no fp16 range limit */
+    FA_DTYPE_FP16_SCALED = 4, /* only as a partial-output type (fa_fwd_v2, fa_fwd_partial,
+                                 fa_combine): fp16 partials scaled per row by a power of two
+                                 (the row's largest |value| below 1), the exponent kept beside
+                                 the lse -- half the traffic of FA_DTYPE_FP32, 11 significant
+                                 bits relative to each row's maximum, no fp16 range limit */
     FA_DTYPE_FP64 = 3        /* IEEE binary64 throughout (the reference's USE_FP64 build,
                                 flash_attention_v1/CUDA/flash_attention_v1.h:29-41): fp64
                                 MFMA, fp64 softmax, fp64 partials and lse */
@@ -174,7 +174,9 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o,
  *   o_part[(row / chunk_rows)][b*H + h][row % chunk_rows][:]   (partial_dtype)
  *   lse   [(row / chunk_rows)][b*H + h][row % chunk_rows]      (fp32; fp64 for FP64)
  * chunk_rows must divide Lq.  chunk_rows = Lq gives a plain [B,H,Lq,d] layout;
- * chunk_rows = Lq / world gives the all-to-all send layout of the multi-GPU path. */
+ * chunk_rows = Lq / world gives the all-to-all send layout of the multi-GPU path.
+ * partial_dtype FA_DTYPE_FP16_SCALED: o_part holds O_row * 2^-e_row in fp16 and lse holds
+ * two floats per row, {lse, e} (lse [...][row % chunk_rows][2]); fa_combine undoes the scale. */
 int fa_fwd_partial(const void* q, const void* k, const void* v,
                    void* o_part, void* lse,
                    int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d,
@@ -191,7 +193,8 @@ int fa_fwd_partial_ex(const void* q, const void* k, const void* v,
                       int64_t chunk_rows, const int64_t* q_strides,
                       int dtype, int partial_dtype, void* stream);
 /* Combine num_splits partials: o_part [num_splits][B*H][L][d] (partial_dtype),
- * lse [num_splits][B*H][L] (fp32, base 2; fp64 for FA_DTYPE_FP64) -> o [B, H, L, d] (dtype), using
+ * lse [num_splits][B*H][L] (fp32, base 2; fp64 for FA_DTYPE_FP64; [num_splits][B*H][L][2]
+ * {lse, e} for FA_DTYPE_FP16_SCALED) -> o [B, H, L, d] (dtype), using
  * O = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M), M = max_s lse_s
  * (the reference's formula, flash_attention_v2/numpy_gpu_like.py:269-288, on
  * normalised partials). */

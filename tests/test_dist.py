@@ -26,18 +26,29 @@ def _free_port():
 
 
 def _oracle_partial(q, k, v, chunk_rows, partial_dtype):
+    """The kernel's layouts; for ops.PARTIAL_FP16_SCALED (include/fa_mi355x.h) the rows are
+    fp16 O * 2^-e with e = frexp exponent of the row's max |O|, lse [..., 2] = {lse, e}."""
     B, H, Lq, d = q.shape
     O, lse = partial_lse(q.double().numpy(), k.double().numpy(), v.double().numpy())
     nch = Lq // chunk_rows
     O = O.reshape(B * H, nch, chunk_rows, d).transpose(1, 0, 2, 3)
     lse = lse.reshape(B * H, nch, chunk_rows).transpose(1, 0, 2)
+    if partial_dtype == "fp16_scaled":
+        e = np.frexp(np.abs(O).max(axis=-1))[1].astype(np.float64)
+        O = np.ldexp(O, -e[..., None].astype(np.int64)).astype(np.float16)
+        lse = np.stack([lse, e], axis=-1)
+        return torch.from_numpy(np.ascontiguousarray(O)), torch.from_numpy(np.ascontiguousarray(lse)).float()
     return (torch.from_numpy(np.ascontiguousarray(O)).to(partial_dtype),
             torch.from_numpy(np.ascontiguousarray(lse)).float())
 
 
 def _oracle_combine(o_part, lse, B, H, dtype):
     S, BH, L, d = o_part.shape
-    O = combine_lse(o_part.double().numpy(), lse.double().numpy())
+    O, lse = o_part.double().numpy(), lse.double().numpy()
+    if lse.ndim == 4:  # scaled fp16 partials: undo 2^-e
+        O = np.ldexp(O, lse[..., 1:].astype(np.int64))
+        lse = lse[..., 0]
+    O = combine_lse(O, lse)
     return torch.from_numpy(O.reshape(B, H, L, d)).to(dtype)
 
 
@@ -49,7 +60,7 @@ def _oracle_partial_chunk(q_rows, k, v, o_out, lse_out, partial_dtype):
     lse_out.copy_(lse[0].to(lse_out.dtype))
 
 
-def _worker(rank, world, port, result_path, overlap):
+def _worker(rank, world, port, result_path, overlap, pdtype):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -62,9 +73,9 @@ def _worker(rank, world, port, result_path, overlap):
     q, k, v = (torch.randn(B, H, L, d, generator=g, dtype=torch.float64) for _ in range(3))
     lo, hi = fdist.shard_bounds(L, world, rank)
     local = fdist.splitkv_attention(q, k[:, :, lo:hi].contiguous(), v[:, :, lo:hi].contiguous(),
-                                    partial_dtype=torch.float64, overlap=overlap)
+                                    partial_dtype=pdtype, overlap=overlap)
     full = fdist.splitkv_attention(q, k[:, :, lo:hi].contiguous(), v[:, :, lo:hi].contiguous(),
-                                   partial_dtype=torch.float64, gather=True, overlap=overlap)
+                                   partial_dtype=pdtype, gather=True, overlap=overlap)
     ref = attention_fp64(q.numpy(), k.numpy(), v.numpy())
     err_local = np.abs(local.numpy() - ref[:, :, lo:hi]).max()
     err_full = np.abs(full.numpy() - ref).max()
@@ -73,16 +84,19 @@ def _worker(rank, world, port, result_path, overlap):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("pdtype", [torch.float64, "fp16_scaled"], ids=["p64", "pf16s"])
 @pytest.mark.parametrize("overlap", [False, True], ids=["all_to_all", "overlapped"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_splitkv_exchange_gloo(tmp_path, world, overlap):
+def test_splitkv_exchange_gloo(tmp_path, world, overlap, pdtype):
     port = _free_port()
     path = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, port, path, overlap), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, port, path, overlap, pdtype), nprocs=world, join=True,
                        start_method="spawn")
+    # fp32 lse as on the GPU; scaled fp16 rows: 2^-11 relative to each row's max (|O| < 4 here)
+    tol = 1e-6 if pdtype == torch.float64 else 4 * 2.0 ** -11
     for r in range(world):
         err_local, err_full, *_ = open(f"{path}.{r}").read().split(" ", 2)
-        assert float(err_local) < 1e-6 and float(err_full) < 1e-6  # fp32 lse, as on the GPU
+        assert float(err_local) < tol and float(err_full) < tol
 
 
 def test_shard_bounds():
