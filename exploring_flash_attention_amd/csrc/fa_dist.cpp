@@ -39,6 +39,10 @@ int core_fail(int st, const char* what) { return fail(st, "%s: %s", what, fa_las
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t esize(int dtype) { return dtype == FA_DTYPE_FP64 ? 8 : dtype == FA_DTYPE_FP32 ? 4 : 2; }
+// lse bytes per row: fp64 for fp64 inputs; {lse, e} for scaled fp16 partials
+size_t lsize(int dtype, int pdtype) {
+    return dtype == FA_DTYPE_FP64 ? 8 : pdtype == FA_DTYPE_FP16_SCALED ? 8 : 4;
+}
 
 struct Layout {
     size_t part_bytes, lse_bytes;  // one side (send or receive)
@@ -49,7 +53,7 @@ Layout layout(int64_t BH, int64_t L, int64_t d, int dtype, int pdtype) {
     Layout w{};
     const size_t rows = (size_t)BH * L;  // W chunks of BH * L/W rows
     w.part_bytes = align256(rows * d * esize(pdtype));
-    w.lse_bytes = align256(rows * (dtype == FA_DTYPE_FP64 ? 8 : 4));
+    w.lse_bytes = align256(rows * lsize(dtype, pdtype));
     w.send_o = 0;
     w.send_lse = w.send_o + w.part_bytes;
     w.recv_o = w.send_lse + w.lse_bytes;
@@ -99,7 +103,8 @@ int fa_fwd_v2_dist_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, in
     if (L % world) return fail(FA_ERR_INVALID_ARG, "L=%lld must be divisible by world=%d", (long long)L, world);
     if (dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_FP16 && dtype != FA_DTYPE_FP64)
         return fail(FA_ERR_UNSUPPORTED, "dtype %d has no kernel", dtype);
-    if (partial_dtype != dtype && !(partial_dtype == FA_DTYPE_FP32 && dtype != FA_DTYPE_FP64))
+    if (partial_dtype != dtype && !((partial_dtype == FA_DTYPE_FP32 || partial_dtype == FA_DTYPE_FP16_SCALED) &&
+                                    dtype != FA_DTYPE_FP64))
         return fail(FA_ERR_UNSUPPORTED, "partial dtype %d not valid for dtype %d", partial_dtype, dtype);
     *bytes = layout(B * H, L, d, dtype, partial_dtype).total;
     return ok();
@@ -128,7 +133,7 @@ int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void
         return core_fail(st, "fa_fwd_partial");
     // 2. chunk p -> rank p (one grouped send/recv round)
     const size_t chunk_o = (size_t)BH * Lc * d * esize(partial_dtype);
-    const size_t chunk_l = (size_t)BH * Lc * (dtype == FA_DTYPE_FP64 ? 8 : 4);
+    const size_t chunk_l = (size_t)BH * Lc * lsize(dtype, partial_dtype);
     if (world > 1) {
         if (ncclResult_t r = ncclGroupStart()) return rccl_fail(r, "ncclGroupStart");
         for (int p = 0; p < world; ++p) {

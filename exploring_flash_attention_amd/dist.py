@@ -226,8 +226,10 @@ def splitkv_attention_native(q, k_shard, v_shard, comm, gather=False, partial_dt
     W = comm.world
     if L % W or k_shard.shape[2] * W != L:
         raise ValueError(f"L={L} must be divisible by world {W} and k_shard must hold L/W keys")
-    # 16-bit partials by default, as splitkv_attention: they halve the exchanged bytes
-    pd = q.dtype if partial_dtype is None else partial_dtype
+    # per-row scaled fp16 partials by default, as splitkv_attention (fp64 for fp64 inputs)
+    if partial_dtype is None:
+        partial_dtype = torch.float64 if q.dtype == torch.float64 else ops.PARTIAL_FP16_SCALED
+    pd = partial_dtype
     nbytes = ctypes.c_size_t()
     _dcheck(dist_lib().fa_fwd_v2_dist_workspace_size(B, H, L, d, W, ops._DTYPES[q.dtype],
                                                      ops._PDTYPES[pd], ctypes.byref(nbytes)))

@@ -43,7 +43,9 @@ int fa_dist_comm_init(void** comm, int world, int rank, const void* id);
 int fa_dist_comm_destroy(void* comm);
 
 /* Workspace of fa_fwd_v2_dist: send + receive partials and lse, plus the all-gather
- * staging buffer.  L must be divisible by world. */
+ * staging buffer.  L must be divisible by world.  partial_dtype (the exchanged format):
+ * the input dtype, FA_DTYPE_FP32 or FA_DTYPE_FP16_SCALED (bf16's bytes, 11 significant
+ * bits; fa_fwd_partial's layout, include/fa_mi355x.h); FA_DTYPE_FP64 for fp64 inputs. */
 int fa_fwd_v2_dist_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int world,
                                   int dtype, int partial_dtype, size_t* bytes);
 

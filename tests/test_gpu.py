@@ -445,6 +445,13 @@ def test_dist_native_rccl_single_rank(gpu):
             o = fdist.splitkv_attention_native(q.to(gpu), k.to(gpu), v.to(gpu), comm, gather=gather)
             torch.cuda.synchronize()
             _gate(o, ref, torch.bfloat16)
+        # every exchange format; the same kernels as the torch.distributed path, bit for bit
+        for pd in (torch.bfloat16, torch.float32, "fp16_scaled"):
+            o = fdist.splitkv_attention_native(q.to(gpu), k.to(gpu), v.to(gpu), comm, partial_dtype=pd)
+            o_py = fdist.splitkv_attention(q.to(gpu), k.to(gpu), v.to(gpu), partial_dtype=pd)
+            torch.cuda.synchronize()
+            _gate(o, ref, torch.bfloat16)
+            assert torch.equal(o, o_py), pd
         q, k, v = _inputs(1, 2, 100, 64, torch.float64, seed=9)
         o = fdist.splitkv_attention_native(q.to(gpu), k.to(gpu), v.to(gpu), comm, gather=True)
         assert np.abs(o.cpu().numpy() - _ref(q, k, v)).max() <= 1e-12
