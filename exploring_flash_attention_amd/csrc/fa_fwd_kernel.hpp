@@ -100,6 +100,12 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 #define FA_MAXNC 1
 #endif
 // packed fp32 softmax arithmetic for d <= FA_PK_MAXD (0 = off)
+// FA_QSCALE_MASK (head-dim bits, d_bit): Q pre-scaled by c = log2(e) * scale once per
+// workgroup (rounded to the input type) and -m splatted into the QK^T accumulators'
+// initial value, so the exponent needs no per-score FMA
+#ifndef FA_QSCALE_MASK
+#define FA_QSCALE_MASK 0x5  // d = 32, 128 (A/B: DESIGN.md §5)
+#endif
 #ifndef FA_PK_MAXD
 #define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
 #endif
@@ -160,6 +166,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     // bounded by 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows
     // (the dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
     constexpr float kThr = 4.f;
+    constexpr bool QSCALE = (FA_QSCALE_MASK & d_bit(D)) != 0;
     constexpr bool FA_MFMA_ROWSUM = D <= FA_MFMA_ROWSUM_MAXD;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -282,7 +289,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     for (int j = 0; j < 8; ++j) ones[j] = static_cast<T>(1.0f);
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-        m[r] = -INFINITY;
+        m[r] = QSCALE ? 0.f : -INFINITY;  // QSCALE: the accumulators start at -m = 0
         l[r] = 0.f;
     }
     const float c = a.scale_log2;
@@ -302,7 +309,17 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2) s[r][b2] = f32x16{};
+            for (int b2 = 0; b2 < NKB; ++b2) {
+                if constexpr (QSCALE) {
+                    const float nm = -m[r];
+                    const double nm2 = __builtin_bit_cast(double, f32x2{nm, nm});
+                    typedef double d8 __attribute__((ext_vector_type(8)));
+                    const d8 v = {nm2, nm2, nm2, nm2, nm2, nm2, nm2, nm2};
+                    s[r][b2] = __builtin_bit_cast(f32x16, v);
+                } else {
+                    s[r][b2] = f32x16{};
+                }
+            }
         rd(0, kf[0]);
 #pragma unroll
         for (int g = 0; g < NKS / G; ++g) {
@@ -336,7 +353,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
                     for (int i = 0; i < 16; i += 2) {
                         f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
-                        x = __builtin_elementwise_fma(x, c2, nm2);
+                        if constexpr (!QSCALE) x = __builtin_elementwise_fma(x, c2, nm2);
                         x[0] = __builtin_amdgcn_exp2f(x[0]);
                         x[1] = __builtin_amdgcn_exp2f(x[1]);
                         s[r][b2][i] = x[0];
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #if FA_ABL_NOEXP
                     s[r][b2][i] = __builtin_fmaf(s[r][b2][i], c, -m[r]);
 #else
-                    s[r][b2][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][b2][i], c, -m[r]));
+                    s[r][b2][i] = __builtin_amdgcn_exp2f(QSCALE ? s[r][b2][i] : __builtin_fmaf(s[r][b2][i], c, -m[r]));
 #endif
                     if (!FA_MFMA_ROWSUM) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
                 }
@@ -393,8 +410,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
                     if (b2 > 0 || i >= 4) mx4[i & 3] = FA_MAXNC ? fmax_nc(mx4[i & 3], s[r][b2][i]) : fmaxf(mx4[i & 3], s[r][b2][i]);
-            mx[r] = FA_MAXNC ? pair_max(fmax_nc(fmax_nc(mx4[0], mx4[1]), fmax_nc(mx4[2], mx4[3]))) * c
-                             : pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * c;
+            // (QSCALE: already in log2 units, relative to m)
+            mx[r] = FA_MAXNC ? pair_max(fmax_nc(fmax_nc(mx4[0], mx4[1]), fmax_nc(mx4[2], mx4[3]))) * (QSCALE ? 1.f : c)
+                             : pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * (QSCALE ? 1.f : c);
         }
     };
     // V^T fragments of (32-key block b2, 32-column block db): 4 transposed reads of 4
@@ -449,6 +467,21 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
+          if constexpr (QSCALE) {
+            // scores (sc, mx) are relative to m (set from tile 0 in the prologue)
+            if (__builtin_amdgcn_ballot_w64(mx[r] > kThr)) {
+                const float delta = fmaxf(mx[r], 0.f);
+                const float alpha = __builtin_amdgcn_exp2f(-delta);
+                m[r] += delta;
+                l[r] *= alpha;
+#pragma unroll
+                for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sc[r][b2][i] -= delta;
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
+            }
+          } else {
             if (__builtin_amdgcn_ballot_w64(mx[r] > m[r] + kThr)) {
                 const float m_new = fmaxf(m[r], mx[r]);
                 const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
@@ -458,6 +491,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
                 for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
             }
+          }
         }
 
 #if FA_DMA_LATE
@@ -558,6 +592,15 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[r][ks]));
+    if constexpr (QSCALE) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qf[r][ks][j] = static_cast<T>(static_cast<float>(qf[r][ks][j]) * c);
+        }
+    }
     __syncthreads();
     FA_STAMP(1);
     f32x16 sa[RB][NKB], sb[RB][NKB];
@@ -565,6 +608,17 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     qk(kring, sa);
     if constexpr (TAIL) mask(0, sa);
     rowmax(sa, mx);
+    if constexpr (QSCALE) {  // m = tile 0's row max; its scores relative to it
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            m[r] = mx[r];
+#pragma unroll
+            for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sa[r][b2][i] -= mx[r];
+            mx[r] = 0.f;
+        }
+    }
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
     FA_STAMP(2);
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--acc", action="store_true", help="also report the error against fp32")
     args = ap.parse_args()
     B, H, L, d = CFG[args.config]
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -57,11 +58,19 @@ def main():
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / args.iters)
     flops = 4.0 * B * H * L * L * d
+    ref = None
+    if args.acc:  # fp32 reference of the first 4 heads (scores materialised)
+        qf, kf, vf = (x[:1, :4].float() for x in (q, k, v))
+        ref = torch.softmax(qf @ kf.transpose(-1, -2) / d ** 0.5, dim=-1) @ vf
     for i, p in enumerate(args.libs):
         med = statistics.median(times[i])
         diff = (outs[i].float() - outs[0].float()).abs().max().item()
+        acc = ""
+        if ref is not None:
+            err = (outs[i][:1, :4].float() - ref).abs()
+            acc = f"  vs_fp32 max {err.max().item():.2e} mean {err.mean().item():.2e}"
         print(f"{p}: median {med * 1e3:.1f} us  min {min(times[i]) * 1e3:.1f} us  "
-              f"{flops / (med * 1e-3) / 1e12:.1f} TFLOP/s  maxdiff_vs_0 {diff:.2e}", flush=True)
+              f"{flops / (med * 1e-3) / 1e12:.1f} TFLOP/s  maxdiff_vs_0 {diff:.2e}{acc}", flush=True)
 
 
 if __name__ == "__main__":

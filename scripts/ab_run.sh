@@ -8,7 +8,7 @@ libs=()
 for n in "$@"; do libs+=("exploring_flash_attention_amd/_lib/ab/$n"); done
 for c in ${CONFIGS:-c3}; do
   echo "== $c"
-  timeout -k 10 240 python scripts/ab.py --config $c --rounds ${ROUNDS:-10} "${libs[@]}" 2>&1 | grep -v amdgpu.ids
+  timeout -k 10 240 python scripts/ab.py --config $c --rounds ${ROUNDS:-10} ${AB_ARGS:-} "${libs[@]}" 2>&1 | grep -v amdgpu.ids
   rc=${PIPESTATUS[0]}
   [ $rc -eq 0 ] || { echo "ab.py exited $rc -- stopping"; exit $rc; }
 done
