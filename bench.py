@@ -132,6 +132,31 @@ def c5_step(torch, fdist, dev, world, rank, impl="torch"):
     return step, kernel, flops(B, H, L, d, Lk=hi - lo)
 
 
+def c5_breakdown(torch, ops, fdist, dev, world, rank, barrier):
+    """C5 on this rank without the exchange: the partial kernels over all L query rows
+    (one launch, all-to-all send layout) and the combine of W received partials for the
+    rank's L/W rows, each timed alone; bytes per rank that cross xGMI."""
+    cc = CONFIGS["c5"]
+    B, H, L, d = cc["B"], cc["H"], cc["L"], cc["d"]
+    lo, hi = fdist.shard_bounds(L, world, rank)
+    Lc = L // world
+    q, _, _ = _make_inputs(torch, dev, B, H, L, d, seed=99)
+    _, k, v = _make_inputs(torch, dev, B, H, 1, d, seed=1000 + rank, Lk=hi - lo)
+    pd = ops.PARTIAL_FP16_SCALED
+    o_part, lse = ops.attention_partial(q, k, v, chunk_rows=Lc, partial_dtype=pd)
+    n = 5
+    _, p_ms = time_step(torch, lambda: ops.attention_partial(q, k, v, chunk_rows=Lc, partial_dtype=pd,
+                                                             o_part=o_part, lse=lse), n, 2, barrier)
+    out = torch.empty(B, H, Lc, d, dtype=q.dtype, device=dev)
+    _, c_ms = time_step(torch, lambda: ops.combine(o_part, lse, B, H, q.dtype, out=out), n, 2, barrier)
+    p_ms, c_ms = p_ms / n, c_ms / n
+    c_bytes = o_part.numel() * 2 + lse.numel() * 4 + out.numel() * 2
+    x_bytes = (world - 1) * (o_part[0].numel() * 2 + lse[0].numel() * 4)
+    return {"partial_ms": round(p_ms, 3), "combine_ms": round(c_ms, 4),
+            "combine_gbps": round(c_bytes / (c_ms * 1e-3) / 1e9, 1),
+            "exchange_bytes_per_rank": int(x_bytes), "partial_format": "fp16 scaled per row"}
+
+
 def load_traffic(config):
     path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     try:
@@ -307,6 +332,13 @@ def main():
                                         "exchange": ("per-chunk partials pipelined with pairwise RCCL "
                                                      "send/recv" if world > 1 else "none")}
             del st5
+            torch.cuda.empty_cache()
+            bd = c5_breakdown(torch, ops, fdist, dev, world, rank, barrier)
+            tb = torch.tensor([bd["partial_ms"], bd["combine_ms"]], device=dev, dtype=torch.float64)
+            if world > 1:
+                dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+            bd["partial_ms"], bd["combine_ms"] = round(float(tb[0]), 3), round(float(tb[1]), 4)
+            extra["c5_splitkv_dist"]["breakdown_max_over_ranks"] = bd
         except Exception as exc:  # noqa: BLE001 -- reported, the headline stands
             extra["c5_splitkv_dist"] = {"error": f"{type(exc).__name__}: {exc}"[:300], "ranks": world}
         torch.cuda.empty_cache()
