@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--acc", action="store_true", help="also report the error against fp32")
+    ap.add_argument("--kvtpb", type=int, default=0, help="time fa_fwd_v2 with this kv_tiles_per_block")
     args = ap.parse_args()
     B, H, L, d = CFG[args.config]
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -34,11 +35,25 @@ def main():
     for p in args.libs:
         h = ctypes.CDLL(p)
         h.fa_fwd_v1.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64] * 4 + [ctypes.c_int, ctypes.c_void_p]
+        h.fa_fwd_v2.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_int64] * 4 + [ctypes.c_int] * 3 +
+                                [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+        h.fa_fwd_v2_workspace_size.argtypes = [ctypes.c_int64] * 4 + [ctypes.c_int] * 3 + [
+            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]
         libs.append(h)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ws = None
+    if args.kvtpb:  # FA-v2 split-KV (in-kernel combine), scaled fp16 partials
+        nb, ns = ctypes.c_size_t(), ctypes.c_int()
+        assert libs[0].fa_fwd_v2_workspace_size(B, H, L, d, args.kvtpb, 1, 4, ctypes.byref(nb), ctypes.byref(ns)) == 0
+        ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
+        print(f"v2: kv_tiles_per_block {args.kvtpb}, {ns.value} splits, workspace {nb.value / 1e9:.2f} GB")
 
     def run(i):
-        st = libs[i].fa_fwd_v1(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d, 1, stream)
+        if ws is not None:
+            st = libs[i].fa_fwd_v2(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d,
+                                   min(32, d), min(32, d), args.kvtpb, ws.data_ptr(), ws.numel(), 1, 4, stream)
+        else:
+            st = libs[i].fa_fwd_v1(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d, 1, stream)
         assert st == 0, st
 
     for i in range(len(libs)):
