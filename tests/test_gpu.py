@@ -331,11 +331,14 @@ def test_running_max_rescale_is_exercised(gpu):
 # partial / combine building blocks
 # ----------------------------------------------------------------------------------------
 
-@pytest.mark.parametrize("pdtype", [torch.float32, torch.bfloat16, "fp16_scaled"], ids=["p32", "pbf16", "pf16s"])
-def test_partial_layout_and_lse(gpu, pdtype):
+@pytest.mark.parametrize("dtype,pdtype", [(torch.bfloat16, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                          (torch.bfloat16, "fp16_scaled"), (torch.float16, "fp16_scaled"),
+                                          (torch.float16, torch.float16)],
+                         ids=["p32", "pbf16", "pf16s", "f16_pf16s", "f16_pf16"])
+def test_partial_layout_and_lse(gpu, dtype, pdtype):
     from exploring_flash_attention_amd import ops
     B, H, Lq, Lk, d, cr = 2, 3, 256, 96, 64, 64
-    q, k, v = _inputs(B, H, Lq, d, torch.bfloat16, seed=11, Lk=Lk)
+    q, k, v = _inputs(B, H, Lq, d, dtype, seed=11, Lk=Lk)
     o_part, lse = ops.attention_partial(q.to(gpu), k.to(gpu), v.to(gpu), chunk_rows=cr,
                                         partial_dtype=pdtype)
     torch.cuda.synchronize()
