@@ -1,0 +1,73 @@
+// MFMA peak microbenchmark (confirm the bf16 dense peak on the box).
+// Every wave issues back-to-back v_mfma_f32_32x32x16_bf16 on 4 independent accumulators
+// (no VALU, no memory in the loop), 2 waves per SIMD on every CU.  Reports the achieved
+// TFLOP/s, the shader clock the chip held (s_memtime cycles over s_memrealtime's 100 MHz
+// wall clock, per workgroup) and the peak those imply (4096 FLOP / clk / CU x CUs x clock).
+//   hipcc -O3 --offload-arch=gfx950 scripts/mfma_peak.hip -o scripts/bin/mfma_peak
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256) void mfma_loop(float* sink, unsigned long long* clk, int iters) {
+    bf16x8 a, b;
+    for (int j = 0; j < 8; ++j) {
+        a[j] = (__bf16)(0.001f * (threadIdx.x + j));
+        b[j] = (__bf16)(0.002f * (threadIdx.x - j));
+    }
+    f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < iters; ++i) {
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c3, 0, 0, 0);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    float s = 0.f;
+    for (int j = 0; j < 16; ++j) s += c0[j] + c1[j] + c2[j] + c3[j];
+    if (s == 12345.678f) sink[threadIdx.x] = s;  // keeps the chain live
+    if (threadIdx.x == 0) {
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+int main() {
+    int dev = 0, ncu = 0, khz = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, dev);
+    const int blocks = ncu * 2;  // 2 x 4 waves per CU = 2 waves per SIMD
+    const int iters = 20000;
+    float* sink;
+    unsigned long long* clk;
+    (void)hipMalloc(&sink, 256 * sizeof(float));
+    (void)hipMalloc(&clk, 2 * blocks * sizeof(unsigned long long));
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int w = 0; w < 20; ++w) mfma_loop<<<blocks, 256>>>(sink, clk, iters);  // clock ramp
+    (void)hipEventRecord(e0);
+    const int reps = 20;
+    for (int r = 0; r < reps; ++r) mfma_loop<<<blocks, 256>>>(sink, clk, iters);
+    (void)hipEventRecord(e1);
+    if (hipEventSynchronize(e1) != hipSuccess) return 1;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long* h = new unsigned long long[2 * blocks];
+    (void)hipMemcpy(h, clk, 2 * blocks * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    double mhz_sum = 0.0;
+    for (int i = 0; i < blocks; ++i) mhz_sum += (double)h[2 * i] / ((double)h[2 * i + 1] / 100.0);
+    const double mhz = mhz_sum / blocks;  // s_memrealtime ticks at 100 MHz
+    const double flops = 2.0 * 32 * 32 * 16 * 4.0 * iters * (blocks * 4.0) * reps;
+    const double tflops = flops / (ms * 1e-3) / 1e12;
+    printf("{\"cus\": %d, \"rated_clock_mhz\": %.0f, \"held_clock_mhz\": %.0f, \"mfma_bf16_tflops\": %.1f, "
+           "\"peak_at_rated_clock_tflops\": %.1f, \"peak_at_held_clock_tflops\": %.1f, "
+           "\"kernel\": \"4 independent v_mfma_f32_32x32x16_bf16 chains per wave, 2 waves per SIMD\"}\n",
+           ncu, khz / 1000.0, mhz, tflops, 4096.0 * ncu * khz * 1e3 / 1e12, 4096.0 * ncu * mhz * 1e6 / 1e12);
+    return 0;
+}
