@@ -104,7 +104,7 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 // workgroup (rounded to the input type) and -m splatted into the QK^T accumulators'
 // initial value, so the exponent needs no per-score FMA
 #ifndef FA_QSCALE_MASK
-#define FA_QSCALE_MASK 0x5  // d = 32, 128 (A/B: DESIGN.md §5)
+#define FA_QSCALE_MASK 0  // off: +2-4 % but peaked rows lose accuracy
 #endif
 #ifndef FA_PK_MAXD
 #define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %

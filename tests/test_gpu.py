@@ -240,6 +240,31 @@ def test_strided_views_without_kernel_layout(gpu):
     assert np.abs(ops.attention_v1(q64, k64, v64).cpu().numpy() - ref).max() <= 1e-12
 
 
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("order", ["rising", "falling"])
+def test_rescale_every_tile(gpu, d, order):
+    """Scores that climb by ~8 (log2 units) per 64-key tile force the defer-max rescale on
+    every tile (rising), or never after the first (falling); peaked rows with scores up to
+    ~130.  Every variant, bf16, against the fp64 oracle.  (d = 32 and 128 run the Q
+    pre-scaled kernels of DESIGN.md §4, d = 64 the FMA form.)"""
+    from exploring_flash_attention_amd import ops
+    B, H, L = 1, 2, 1000
+    q, k, v = _inputs(B, H, L, d, torch.float32, seed=31)
+    ramp = torch.arange(L, dtype=torch.float32) / 16.0
+    if order == "falling":
+        ramp = ramp.flip(0)
+    q[..., 0] = 16.0 * (d / 128) ** 0.5  # same climb per tile whatever 1/sqrt(d)
+    k[..., 0] = ramp
+    q, k, v = (x.to(torch.bfloat16) for x in (q, k, v))
+    ref = _ref(q, k, v)
+    qg, kg, vg = q.to(gpu), k.to(gpu), v.to(gpu)
+    for fn in (ops.attention_v1, lambda a, b, c: ops.attention_tiled_d(a, b, c, min(32, d), min(32, d)),
+               lambda a, b, c: ops.attention_v2(a, b, c, 1)):
+        o = fn(qg, kg, vg)
+        torch.cuda.synchronize()
+        _gate(o, ref, torch.bfloat16)
+
+
 def test_empty_inputs(gpu):
     """L = 0 (and B = 0): the reference's NumPy functions return an empty O
     (flash_attention_v1/numpy_basic.py:79-103 never enters its loops); so do these, without
