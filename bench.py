@@ -76,6 +76,44 @@ def cpu_baseline(L, d, heads):
     }
 
 
+_OMP_SNIPPET = r"""
+import ctypes, json, sys, time
+import numpy as np
+lib = ctypes.CDLL(sys.argv[1])
+P, I = ctypes.c_void_p, ctypes.c_int
+lib.oracle_standard_attention.argtypes = [P, P, P, P, I, I, I, I, I]
+H, L, d = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+rng = np.random.default_rng(0)
+q, k, v = (rng.uniform(-1, 1, (1, H, L, d)).astype(np.float32) for _ in range(3))
+o = np.empty_like(q)
+t0 = time.perf_counter()
+lib.oracle_standard_attention(q.ctypes.data, k.ctypes.data, v.ctypes.data, o.ctypes.data, 1, H, L, d, 2)
+print(json.dumps({"wall": time.perf_counter() - t0}))
+"""
+
+
+def cpu_baseline_openmp(L, d, threads):
+    """The C/OpenMP restatement of the reference's standard_attention_cpu
+    (common/standard.h:28-102; oracle/standard_attention.c) over 4 heads per thread of the
+    same shape, fp32, in a child process with OMP_NUM_THREADS = threads."""
+    import subprocess
+    lib = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(lib):
+        return None
+    heads = 4 * threads
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    try:
+        out = subprocess.run([sys.executable, "-c", _OMP_SNIPPET, lib, str(heads), str(L), str(d)],
+                             env=env, capture_output=True, text=True, timeout=120, check=True)
+        wall = json.loads(out.stdout.strip().splitlines()[-1])["wall"]
+    except (subprocess.SubprocessError, ValueError, IndexError, KeyError):
+        return None
+    return {"value": round(heads * flops(1, 1, L, d) / wall / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
+            "kind": "port", "sample": (f"{heads} heads of L={L} d={d} (fp32), naive attention with OpenMP over "
+                                       f"heads; wall {wall:.2f} s; restatement of common/standard.h "
+                                       f"standard_attention_cpu (oracle/standard_attention.c)")}
+
+
 # ------------------------------------------------------------------------------------
 # GPU timing
 # ------------------------------------------------------------------------------------
@@ -198,6 +236,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "heads":
         heads = args.cpu_heads or min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(L, d, heads)  # before any GPU initialisation (fork-safe)
+        omp = cpu_baseline_openmp(L, d, heads)
+        if omp is not None:
+            cpu["openmp_standard_attention"] = omp
 
     import torch
     import torch.distributed as dist
