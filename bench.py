@@ -94,13 +94,14 @@ print(json.dumps({"wall": time.perf_counter() - t0}))
 
 def cpu_baseline_openmp(L, d, threads):
     """The C/OpenMP restatement of the reference's standard_attention_cpu
-    (common/standard.h:28-102; oracle/standard_attention.c) over 4 heads per thread of the
-    same shape, fp32, in a child process with OMP_NUM_THREADS = threads."""
+    (common/standard.h:28-102; oracle/standard_attention.c) over 16 heads per thread of the
+    same shape (the whole C3 batch of 256 heads at 16 threads), fp32, in a child process with
+    OMP_NUM_THREADS = threads."""
     import subprocess
     lib = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
     if not os.path.exists(lib):
         return None
-    heads = 4 * threads
+    heads = min(256, 16 * threads)
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     try:
         out = subprocess.run([sys.executable, "-c", _OMP_SNIPPET, lib, str(heads), str(L), str(d)],
