@@ -13,7 +13,8 @@ Prints ONE JSON line on rank 0 with the metric, the MFMA roofline of the forward
 (achieved = 4*B*H*L^2*d FLOPs per launch / average launch time from HIP events on the
 launch stream) and the CPU baseline: the oracle's restatement of the reference's
 flash_attention_v1/numpy_gpu_like_opt2.py (fp64, Bq=Bk=8) timed on a bounded sample of the
-same workload's heads, one head per process, on the host cores.
+same workload's heads, one head per process, on the host cores (and, beside it, the C/OpenMP
+restatement of the drivers' standard_attention_cpu on the same cores).
 """
 import argparse
 import json
