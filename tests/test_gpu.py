@@ -266,8 +266,15 @@ def test_rescale_every_tile(gpu, d, order, dtype):
     emu = ((p.to(dtype).double() @ v.double()) / p.sum(-1, keepdim=True)).to(dtype).double()
     emu_err = (emu - torch.from_numpy(ref)).abs().max().item()
     qg, kg, vg = q.to(gpu), k.to(gpu), v.to(gpu)
+
+    def sharded(a, b, c, W=4):  # the multi-GPU row-layout path on one GPU: scaled fp16 partials
+        parts = [ops.attention_partial(a, b[:, :, j * L // W:(j + 1) * L // W].contiguous(),
+                                       c[:, :, j * L // W:(j + 1) * L // W].contiguous(),
+                                       partial_dtype=ops.PARTIAL_FP16_SCALED) for j in range(W)]
+        return ops.combine(torch.cat([x[0] for x in parts]), torch.cat([x[1] for x in parts]), B, H, dtype)
+
     for fn in (ops.attention_v1, lambda a, b, c: ops.attention_tiled_d(a, b, c, min(32, d), min(32, d)),
-               lambda a, b, c: ops.attention_v2(a, b, c, 1)):
+               lambda a, b, c: ops.attention_v2(a, b, c, 1), sharded):
         o = fn(qg, kg, vg)
         torch.cuda.synchronize()
         err = np.abs(o.double().cpu().numpy() - ref).max()
