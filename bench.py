@@ -11,10 +11,11 @@ are independent units: weak scaling, no collective in the data path).
 
 Prints ONE JSON line on rank 0 with the metric, the MFMA roofline of the forward kernel
 (achieved = 4*B*H*L^2*d FLOPs per launch / average launch time from HIP events on the
-launch stream) and the CPU baseline: the oracle's restatement of the reference's
-flash_attention_v1/numpy_gpu_like_opt2.py (fp64, Bq=Bk=8) timed on a bounded sample of the
-same workload's heads, one head per process, on the host cores (and, beside it, the C/OpenMP
-restatement of the drivers' standard_attention_cpu on the same cores).
+launch stream), a check of the headline output against fp64 attention on sampled heads, and
+the CPU baseline: the oracle's restatement of the reference's
+flash_attention_v1/numpy_gpu_like_opt2.py (fp64, Bq=Bk=8) timed on k heads per usable host
+core, one head per process, extrapolated to the whole batch (and, beside it, the C/OpenMP
+restatement of the drivers' standard_attention_cpu over the whole batch on the same cores).
 """
 import argparse
 import json
@@ -57,23 +58,62 @@ def _cpu_head(args):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(L, d, heads):
+def host_cores():
+    """(cores this process may use, os.cpu_count()): the CPU affinity set, capped by the
+    cgroup CPU quota (cpu.max) where one is set -- on a GPU box os.cpu_count() reports the
+    whole machine, of which a job gets a share."""
+    n = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else n
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return usable, n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(L, d, ncores, k=1, total_heads=256):
+    """the oracle's restatement of numpy_gpu_like_opt2.py (fp64, Bq=Bk=8)
+    over k heads per core, one head per process on multiprocessing.Pool(ncores); the per-head
+    cost is shape-determined, so the whole batch's time is extrapolated linearly."""
     import multiprocessing as mp
     for var in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
         os.environ[var] = "1"
+    heads = min(total_heads, k * ncores)
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
-    with ctx.Pool(heads) as pool:
+    with ctx.Pool(ncores) as pool:
         per_head = pool.map(_cpu_head, [(L, d, s) for s in range(heads)])
     wall = time.perf_counter() - t0
+    head_s = sum(per_head) / heads
+    extrap = wall * total_heads / heads
+    _, all_cpus = host_cores()
     return {
         "value": round(heads * flops(1, 1, L, d) / wall / 1e9, 4),
         "unit": "GFLOP/s",
-        "cores": heads,
+        "cores": ncores,
         "kind": "port",
-        "sample": (f"{heads} heads of L={L} d={d} (fp64, Bq=Bk=8), one head per process on "
-                   f"{heads} host cores; wall {wall:.1f} s, {sum(per_head) / heads:.1f} s per head; "
-                   f"restatement of flash_attention_v1/numpy_gpu_like_opt2.py (oracle/fa_v1.py)"),
+        "cpu_model": cpu_model(),
+        "host_cpus": all_cpus,
+        "heads_per_core": k,
+        "per_head_s": round(head_s, 2),
+        "extrapolated_s": round(extrap, 1),
+        "sample": (f"{heads} of the {total_heads} heads of L={L} d={d} (fp64, Bq=Bk=8), k={k} per core, one "
+                   f"head per process on Pool({ncores}) ({ncores} usable of {all_cpus} host CPUs, "
+                   f"{cpu_model()}); wall {wall:.1f} s, {head_s:.1f} s per head, all {total_heads} heads "
+                   f"extrapolated to {extrap:.0f} s; restatement of "
+                   f"flash_attention_v1/numpy_gpu_like_opt2.py (oracle/fa_v1.py)"),
     }
 
 
@@ -93,16 +133,16 @@ print(json.dumps({"wall": time.perf_counter() - t0}))
 """
 
 
-def cpu_baseline_openmp(L, d, threads):
+def cpu_baseline_openmp(L, d, threads, total_heads=256):
     """The C/OpenMP restatement of the reference's standard_attention_cpu
-    (common/standard.h:28-102; oracle/standard_attention.c) over 16 heads per thread of the
-    same shape (the whole C3 batch of 256 heads at 16 threads), fp32, in a child process with
-    OMP_NUM_THREADS = threads."""
+    (common/standard.h:28-102; oracle/standard_attention.c) over the whole batch of the same
+    shape (256 heads at C3), fp32, in a child process with OMP_NUM_THREADS = threads
+    (SURVEY.md 8(d))."""
     import subprocess
     lib = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
     if not os.path.exists(lib):
         return None
-    heads = min(256, 16 * threads)
+    heads = total_heads
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     try:
         out = subprocess.run([sys.executable, "-c", _OMP_SNIPPET, lib, str(heads), str(L), str(d)],
@@ -111,9 +151,10 @@ def cpu_baseline_openmp(L, d, threads):
     except (subprocess.SubprocessError, ValueError, IndexError, KeyError):
         return None
     return {"value": round(heads * flops(1, 1, L, d) / wall / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
-            "kind": "port", "sample": (f"{heads} heads of L={L} d={d} (fp32), naive attention with OpenMP over "
-                                       f"heads; wall {wall:.2f} s; restatement of common/standard.h "
-                                       f"standard_attention_cpu (oracle/standard_attention.c)")}
+            "kind": "port", "wall_s": round(wall, 2),
+            "sample": (f"all {heads} heads of L={L} d={d} (fp32), naive attention with OpenMP over heads at "
+                       f"OMP_NUM_THREADS={threads}; wall {wall:.2f} s; restatement of common/standard.h "
+                       f"standard_attention_cpu (oracle/standard_attention.c)")}
 
 
 # ------------------------------------------------------------------------------------
@@ -207,6 +248,51 @@ def load_traffic(config):
         return None
 
 
+def sample_heads(B, H, n=16):
+    """n (b, h) pairs spread over the batch, first and last included."""
+    BH = B * H
+    idx = sorted({round(i * (BH - 1) / (n - 1)) for i in range(n)})
+    return [(i // H, i % H) for i in idx]
+
+
+def output_check(torch, q, k, v, out, n=16):
+    """max_abs / mean_rel of the kernel's output against fp64 attention computed by torch on
+    the device, over n sampled heads (every query tile of each), outside the timed region.
+    (A torch fp64 reference of the same op: the CPU oracle stays out of the product bench.)"""
+    B, H, L, d = q.shape
+    worst, rel_sum, rel_n = 0.0, 0.0, 0
+    for b, h in sample_heads(B, H, n):
+        qq, kk, vv = (t[b, h].double() for t in (q, k, v))
+        p = torch.softmax((qq @ kk.T) / d ** 0.5, dim=-1)
+        ref = p @ vv
+        err = (out[b, h].double() - ref).abs()
+        worst = max(worst, float(err.max()))
+        big = ref.abs() > 1e-3
+        rel_sum += float((err[big] / ref.abs()[big]).sum())
+        rel_n += int(big.sum())
+    return {"max_abs": round(worst, 6), "mean_rel": round(rel_sum / max(rel_n, 1), 6), "heads": n,
+            "reference": "torch fp64 softmax(q k^T / sqrt(d)) v on the device, sampled heads incl. first/last"}
+
+
+WATCHDOG_EXIT = 3
+
+
+def start_watchdog(seconds, rank, partial_line):
+    """After `seconds`: print partial_line() (rank 0's JSON line with the error recorded, or
+    None) and leave the process with status WATCHDOG_EXIT -- a hung exchange is a failed run
+    for the driver, never a green one.  Returns the timer (cancel() it when done)."""
+    def fire():
+        rec = partial_line()
+        if rec is not None:
+            print(json.dumps(rec), flush=True)
+        print(f"bench: watchdog fired after {seconds} s on rank {rank}", file=sys.stderr, flush=True)
+        os._exit(WATCHDOG_EXIT)
+    dog = threading.Timer(seconds, fire)
+    dog.daemon = True
+    dog.start()
+    return dog
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,7 +306,7 @@ def main():
     ap.add_argument("--dist-impl", default="torch", choices=["torch", "native"],
                     help="splitkv-dist exchange: torch.distributed all_to_all, or the C ABI "
                          "fa_fwd_v2_dist (own RCCL communicator, grouped send/recv)")
-    ap.add_argument("--cpu-heads", type=int, default=0, help="CPU baseline sample (0 = min(16, cores))")
+    ap.add_argument("--cpu-cores", type=int, default=0, help="CPU baseline pool size (0 = the usable host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the per-variant extra timings")
     args = ap.parse_args()
@@ -236,9 +322,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "heads":
-        heads = args.cpu_heads or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(L, d, heads)  # before any GPU initialisation (fork-safe)
-        omp = cpu_baseline_openmp(L, d, heads)
+        ncores = args.cpu_cores or host_cores()[0]
+        cpu = cpu_baseline(L, d, ncores)  # before any GPU initialisation (fork-safe)
+        omp = cpu_baseline_openmp(L, d, ncores)
         if omp is not None:
             cpu["openmp_standard_attention"] = omp
 
@@ -258,6 +344,35 @@ def main():
             dist.barrier()
 
     extra = {}
+    if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
+        # per-variant timings at N=1 (informational; not the headline value).  They run
+        # before the headline, so the headline's window also finds the clock settled.
+        # (C3's tiled-d form is the same launch as the headline: fa_fwd_v1_tiled_d validates
+        # the d tiles and runs the fused kernel)
+        for name, c, fn in (("c2_fused", "c2", "v1"), ("c4_splitkv", "c4", "v2"),
+                            ("c4_splitkv_auto", "c4", "v2auto")):
+            cc = CONFIGS[c]
+            qq, kk, vv = _make_inputs(torch, dev, cc["B"], cc["H"], cc["L"], cc["d"], seed=7)
+            if fn == "v1":
+                def st():
+                    ops.attention_v1(qq, kk, vv)
+            else:  # KV_TILES_PER_BLOCK = 4 as in C4, or the occupancy-chosen split
+                kvt = 4 if fn == "v2" else "auto"
+                nb, nsp = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
+                wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
+
+                def st():
+                    ops.attention_v2(qq, kk, vv, kvt, workspace=wsx)
+            n = 50
+            _, ems = time_step(torch, st, n, 20, barrier)
+            f = flops(cc["B"], cc["H"], cc["L"], cc["d"])
+            extra[name] = {"ms": round(ems / n, 4), "tflops": round(f / (ems / n * 1e-3) / 1e12, 1)}
+            if fn.startswith("v2"):
+                extra[name]["splits"] = nsp
+            del qq, kk, vv
+        torch.cuda.empty_cache()
+
+    check = None
     if args.mode == "heads":
         q, k, v = _make_inputs(torch, dev, B, H, L, d, seed=1234 + rank)
         out = torch.empty_like(q)
@@ -274,8 +389,11 @@ def main():
             kernel = "fa_fwd_kernel (split-KV, in-kernel combine)"
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         work = flops(B, H, L, d)
-        workload = f"FA-{'v1 fused' if cfg['variant'] == 'v1' else 'v2 split-KV'} forward"
+        workload = ("FA-v1 fused / tiled-d forward (one kernel)" if cfg["variant"] == "v1"
+                    else "FA-v2 split-KV forward")
         parallel = f"heads{world}" if world > 1 else "single"
+        if rank == 0:
+            check = output_check(torch, q, k, v, out)
     else:
         # C5: keys of one L=16384 sequence sharded over the ranks; all-to-all combine.
         step, kernel, work = c5_step(torch, fdist, dev, world, rank, args.dist_impl)  # work: this rank's share
@@ -292,40 +410,14 @@ def main():
     total_work = work * world
     value = total_work / (wall / args.steps) / 1e9
 
-    if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
-        # per-variant timings at N=1 (informational; not the headline value)
-        for name, c, fn in (("c3_tiled_d", "c3", "tiled_d"), ("c2_fused", "c2", "v1"),
-                            ("c4_splitkv", "c4", "v2"), ("c4_splitkv_auto", "c4", "v2auto")):
-            cc = CONFIGS[c]
-            qq, kk, vv = _make_inputs(torch, dev, cc["B"], cc["H"], cc["L"], cc["d"], seed=7)
-            if fn == "tiled_d":
-                def st():
-                    ops.attention_tiled_d(qq, kk, vv, 32, 32)
-            elif fn == "v1":
-                def st():
-                    ops.attention_v1(qq, kk, vv)
-            else:  # KV_TILES_PER_BLOCK = 4 as in C4, or the occupancy-chosen split
-                kvt = 4 if fn == "v2" else "auto"
-                nb, nsp = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
-                wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
-
-                def st():
-                    ops.attention_v2(qq, kk, vv, kvt, workspace=wsx)
-            n = 20
-            _, ems = time_step(torch, st, n, 5, barrier)
-            f = flops(cc["B"], cc["H"], cc["L"], cc["d"])
-            extra[name] = {"ms": round(ems / n, 4), "tflops": round(f / (ems / n * 1e-3) / 1e12, 1)}
-            if fn.startswith("v2"):
-                extra[name]["splits"] = nsp
-            del qq, kk, vv
-
     if rank == 0:
         avg_ms = ev_ms / args.steps
         achieved = work / (avg_ms * 1e-3) / 1e12
-        traffic = load_traffic(args.config if args.mode == "heads" else "c5")
+        tcfg = args.config if args.mode == "heads" else "c5"
+        traffic = load_traffic(tcfg)
         line = {
             "metric": "flash-attn fwd GFLOP/s (B=32,H=8,L=1024,d=128; % MFMA roofline)"
-            if args.mode == "heads" and args.config == "c3" else f"flash-attn fwd GFLOP/s ({args.config if args.mode == 'heads' else 'c5'})",
+            if args.mode == "heads" and args.config == "c3" else f"flash-attn fwd GFLOP/s ({tcfg})",
             "value": round(value, 1),
             "unit": "GFLOP/s",
             "n_gpus": world,
@@ -342,25 +434,28 @@ def main():
                        "tiles": {"bq": 128, "bk": 64, "threads": 256}},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                         "traffic": traffic, "kernel": kernel,
-                         "kernel_ms": round(avg_ms, 5)},
+                         "traffic": traffic,
+                         "traffic_source": (f"profiles/hbm_traffic.json[{tcfg}] (rocprofv3 PMC passes, "
+                                            "per launch; not measured in this run)") if traffic else None,
+                         "kernel": kernel, "kernel_ms": round(avg_ms, 5)},
             "cpu_baseline": cpu,
         }
+        if check is not None:
+            line["check"] = check
     printed, dog = False, None
     if not args.no_extra and args.mode == "heads":
         # C5 split-KV over all ranks (north_star: 1/2/4/8-GPU split-KV throughput and achieved
         # fraction); every rank takes part in the exchange, time = max over ranks.  A watchdog
         # keeps an exchange that never completes from costing the headline line: after
-        # C5_TIMEOUT_S every rank leaves, rank 0 printing what was measured.
-        def _give_up():
+        # C5_TIMEOUT_S rank 0 prints what was measured, and every rank exits with status 3
+        # (a hang is a failure, never a green run).
+        def _partial_line():
             if rank == 0 and not printed:
                 extra["c5_splitkv_dist"] = {"error": f"no result within {C5_TIMEOUT_S} s", "ranks": world}
                 line["extra"] = extra
-                print(json.dumps(line), flush=True)
-            os._exit(0)
-        dog = threading.Timer(C5_TIMEOUT_S, _give_up)
-        dog.daemon = True
-        dog.start()
+                return line
+            return None
+        dog = start_watchdog(C5_TIMEOUT_S, rank, _partial_line)
         try:
             st5, _, w5 = c5_step(torch, fdist, dev, world, rank)
             n5 = 10
@@ -391,10 +486,10 @@ def main():
             line["extra"] = extra
         print(json.dumps(line), flush=True)
         printed = True
-    if world > 1:
-        dist.destroy_process_group()
     if dog is not None:
         dog.cancel()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

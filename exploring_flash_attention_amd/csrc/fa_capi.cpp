@@ -309,6 +309,12 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
     int kvps;
     const int ns = splits_for(L, d, kv_tiles_per_block, &kvps, e);
+    // one workgroup per (query tile, split, b*h): the grid and the kernel's block index are
+    // 32-bit (dim3, xcd_remap), so a grid past 2^31-1 is refused instead of truncated
+    const int64_t nqt = (L + rows_per_block(e) - 1) / rows_per_block(e);
+    if (B * H * nqt > (int64_t)0x7fffffff / ns)
+        return fail(FA_ERR_UNSUPPORTED, "split-KV grid of %lld x %d workgroups exceeds 2^31-1 "
+                    "(raise kv_tiles_per_block)", (long long)(B * H * nqt), ns);
     const V2Layout w = v2_layout(B * H, L, d, ns, pe);
     *bytes = w.total;
     if (num_splits) *num_splits = ns;
@@ -411,6 +417,10 @@ int fa_fwd_partial_ex(const void* q, const void* k, const void* v, void* o_part,
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (int st = check_ptrs(q, k, v, o_part)) return st;
     if (!lse) return fail(FA_ERR_INVALID_ARG, "lse is NULL");
+    // lse element: fp32, {lse, e} float pairs for scaled fp16 partials, fp64 for fp64 inputs
+    if ((uintptr_t)lse & (pe == fa::Elem::F16S || e == fa::Elem::F64 ? 7 : 3))
+        return fail(FA_ERR_INVALID_ARG, "lse must be aligned to its element (%d bytes)",
+                    pe == fa::Elem::F16S || e == fa::Elem::F64 ? 8 : 4);
     if (chunk_rows <= 0 || Lq % chunk_rows)
         return fail(FA_ERR_INVALID_ARG, "chunk_rows=%lld must divide Lq=%lld", (long long)chunk_rows,
                     (long long)Lq);
@@ -434,6 +444,12 @@ int fa_combine(const void* o_part, const void* lse, void* o, int64_t num_splits,
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (!o_part || !lse || !o) return fail(FA_ERR_INVALID_ARG, "null pointer");
+    // the combine kernel moves 16 bytes per lane through o_part and o
+    if (((uintptr_t)o_part | (uintptr_t)o) & 15)
+        return fail(FA_ERR_INVALID_ARG, "o_part and o must be 16-byte aligned");
+    if ((uintptr_t)lse & (pe == fa::Elem::F16S || e == fa::Elem::F64 ? 7 : 3))
+        return fail(FA_ERR_INVALID_ARG, "lse must be aligned to its element (%d bytes)",
+                    pe == fa::Elem::F16S || e == fa::Elem::F64 ? 8 : 4);
     if (num_splits <= 0 || num_splits > 65536)
         return fail(FA_ERR_INVALID_ARG, "num_splits=%lld out of range", (long long)num_splits);
     fa::CombineArgs c{};

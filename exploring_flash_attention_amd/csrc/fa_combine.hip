@@ -38,14 +38,20 @@ __global__ __launch_bounds__(256) void fa_combine_kernel(CombineArgs a) {
     constexpr bool SCALED = std::is_same_v<PT, f16s_t>;
     constexpr int LS = SCALED ? 2 : 1;
     float mx = -INFINITY;
-    for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, a.lse[LS * (s * a.rows + row)]);
+    // scaled partials: the weights carry 2^(e_s - E), E = the largest exponent, and 2^E is
+    // applied after the division (2^e_s itself overflows fp32 for rows near the bf16 maximum)
+    int emax = -1000;
+    for (int s = 0; s < a.nsplit; ++s) {
+        mx = fmaxf(mx, a.lse[LS * (s * a.rows + row)]);
+        if constexpr (SCALED) emax = max(emax, (int)a.lse[2 * (s * a.rows + row) + 1]);
+    }
 
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float wsum = 0.f;
     for (int s = 0; s < a.nsplit; ++s) {
         float wgt = __builtin_amdgcn_exp2f(a.lse[LS * (s * a.rows + row)] - mx);
         wsum += wgt;
-        if constexpr (SCALED) wgt = __builtin_amdgcn_ldexpf(wgt, (int)a.lse[2 * (s * a.rows + row) + 1]);
+        if constexpr (SCALED) wgt = __builtin_amdgcn_ldexpf(wgt, (int)a.lse[2 * (s * a.rows + row) + 1] - emax);
         const int64_t base = ((int64_t)s * a.rows + row) * D + c8;
         if constexpr (sizeof(PT) == 4) {
             const f32x4 x0 = *(const f32x4*)((const float*)a.o_part + base);
@@ -65,11 +71,11 @@ __global__ __launch_bounds__(256) void fa_combine_kernel(CombineArgs a) {
         }
     }
     const float inv = 1.f / wsum;
+    auto fin = [&](float x) { return SCALED ? __builtin_amdgcn_ldexpf(x * inv, emax) : x * inv; };
     u32x4 out;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        out[j] = (unsigned)from_f<T>(acc[2 * j] * inv) |
-                 ((unsigned)from_f<T>(acc[2 * j + 1] * inv) << 16);
+        out[j] = (unsigned)from_f<T>(fin(acc[2 * j])) | ((unsigned)from_f<T>(fin(acc[2 * j + 1])) << 16);
     *(u32x4*)((unsigned short*)a.o + row * D + c8) = out;
 }
 

@@ -136,11 +136,19 @@ int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void
     const size_t chunk_l = (size_t)BH * Lc * lsize(dtype, partial_dtype);
     if (world > 1) {
         if (ncclResult_t r = ncclGroupStart()) return rccl_fail(r, "ncclGroupStart");
+        const ncclComm_t c = (ncclComm_t)comm;
         for (int p = 0; p < world; ++p) {
-            ncclSend(ws + w.send_o + p * chunk_o, chunk_o, ncclUint8, p, (ncclComm_t)comm, s);
-            ncclRecv(ws + w.recv_o + p * chunk_o, chunk_o, ncclUint8, p, (ncclComm_t)comm, s);
-            ncclSend(ws + w.send_lse + p * chunk_l, chunk_l, ncclUint8, p, (ncclComm_t)comm, s);
-            ncclRecv(ws + w.recv_lse + p * chunk_l, chunk_l, ncclUint8, p, (ncclComm_t)comm, s);
+            ncclResult_t r = ncclSend(ws + w.send_o + p * chunk_o, chunk_o, ncclUint8, p, c, s);
+            if (r == ncclSuccess) r = ncclRecv(ws + w.recv_o + p * chunk_o, chunk_o, ncclUint8, p, c, s);
+            if (r == ncclSuccess) r = ncclSend(ws + w.send_lse + p * chunk_l, chunk_l, ncclUint8, p, c, s);
+            if (r == ncclSuccess) r = ncclRecv(ws + w.recv_lse + p * chunk_l, chunk_l, ncclUint8, p, c, s);
+            if (r != ncclSuccess) {
+                // close the group before reporting: an open group would swallow the next call
+                (void)ncclGroupEnd();
+                char what[64];
+                snprintf(what, sizeof what, "send/recv with rank %d", p);
+                return rccl_fail(r, what);
+            }
         }
         if (ncclResult_t r = ncclGroupEnd()) return rccl_fail(r, "send/recv exchange");
     }

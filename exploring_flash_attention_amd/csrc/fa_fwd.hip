@@ -35,7 +35,6 @@ static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s) {
     if (a.strided) return launch_fwd_strided(t, pt, d, mode, a, s);
     if (FA_W64 && mode == kFinal && d == 128) return launch_fwd_w64(t, a, s);
-    if (FA_PERSIST && mode == kFinal && d <= 128) return launch_fwd_persist(t, d, a, s);
     if (mode == kFinal) {
         if (t == Elem::BF16) return launch_d<__bf16, __bf16, kFinal>(d, a, s);
         if (t == Elem::F16) return launch_d<_Float16, _Float16, kFinal>(d, a, s);

@@ -803,13 +803,19 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             float M = lse_own[r];
-            for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, load_lse(sp, r));
+            // scaled partials: weights carry 2^(e - E), E the largest exponent of the row's
+            // splits, and 2^E is applied after the division (2^e overflows near bf16's max)
+            float E = -1000.f;
+            for (int sp = 0; sp < ns; ++sp) {
+                M = fmaxf(M, load_lse(sp, r));
+                if constexpr (SCALED) E = fmaxf(E, load_esc(sp, r));
+            }
             float wsum = 0.f;
             f32x16 acc[NDB];
 #pragma unroll
             for (int db = 0; db < NDB; ++db) acc[db] = f32x16{};
             auto fma_split = [&](const frag_t (&fr)[NF], float w, float es) {
-                const float wv = SCALED ? __builtin_amdgcn_ldexpf(w, (int)es) : w;
+                const float wv = SCALED ? __builtin_amdgcn_ldexpf(w, (int)(es - E)) : w;
 #pragma unroll
                 for (int f = 0; f < NF; ++f)
 #pragma unroll
@@ -840,8 +846,16 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                 }
             }
             const int64_t q_row = q_row0 + 32 * r;
+            float inv_w = 1.f / wsum;
+            if constexpr (SCALED) {
+#pragma unroll
+                for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) acc[db][i] = __builtin_amdgcn_ldexpf(acc[db][i] * inv_w, (int)E);
+                inv_w = 1.f;
+            }
             if (q_row < a.Lq)
-                store_row((unsigned short*)a.o_final + o_head + q_row * orow, acc, 1.f / wsum);
+                store_row((unsigned short*)a.o_final + o_head + q_row * orow, acc, inv_w);
         }
     } else {
 #pragma unroll

@@ -78,7 +78,6 @@ struct FwdArgs {
     // fp64 mode (fa_fwd64.hip)
     double scale_log2_64;    // log2(e) / sqrt(d) in double
     double* lse64;           // partial only: log2-sum-exp per row (double)
-    unsigned sched_epoch;    // persistent kernel: selects its work-queue set (fa_fwd_persist.hip)
     // strided tensors (final and fused split modes of fa_fwd_kernel): element strides of
     // (batch, head, row); d is contiguous and V shares K's strides.  strided == 0: contiguous
     // [B, H, L, d] and these are unused.
@@ -114,13 +113,6 @@ int fwd_lds_bytes(int d);
 #define FA_W64 0  // measured: steady state equal to fa_fwd_kernel, per-item seam 1.5x
 #endif
 hipError_t launch_fwd_w64(Elem t, const FwdArgs& a, hipStream_t s);
-// persistent final-mode forward with per-XCD work queues, d = 32 / 64 / 128
-// (fa_fwd_persist.hip); FA_PERSIST selects it for fa_fwd_v1 / fa_fwd_v1_tiled_d
-#ifndef FA_PERSIST
-#define FA_PERSIST 0
-#endif
-hipError_t launch_fwd_persist(Elem t, int d, const FwdArgs& a, hipStream_t s);
-int persist_rows_per_item();
 int w64_rows_per_block();
 // fp64 mode (fa_fwd64.hip): 64 query rows x 16-key tiles; final or row-layout partial
 hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);

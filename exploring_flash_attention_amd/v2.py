@@ -59,19 +59,20 @@ def flash_attention_v2(Q, K, V, O=None, B=None, H=None, L=None, d=None, d_tile_q
 
 
 def _v2_dist(Q, K, V, world_size, group, partial_dtype):
-    import torch
     import torch.distributed as tdist
 
     from . import dist as fadist
-    assert _host.is_device_tensor(Q) and Q.dim() == 4, \
+    import torch
+    assert isinstance(Q, torch.Tensor) and Q.dim() == 4, \
         "world_size > 1 takes [B, H, L, d] device tensors (one process per GPU)"
     W = tdist.get_world_size(group)
     assert W == world_size, f"world_size={world_size} but the process group has {W} ranks"
     rank = tdist.get_rank(group)
     lo, hi = fadist.shard_bounds(Q.shape[2], W, rank)
+    # partial_dtype None: splitkv_attention's default (per-row scaled fp16, fp64 for fp64
+    # inputs) -- the same exchange format as every other multi-GPU entry point
     return fadist.splitkv_attention(Q, K[:, :, lo:hi].contiguous(), V[:, :, lo:hi].contiguous(),
-                                    group=group, gather=True,
-                                    partial_dtype=torch.float32 if partial_dtype is None else partial_dtype)
+                                    group=group, gather=True, partial_dtype=partial_dtype)
 
 
 flash_attention_v2_opt = flash_attention_v2

@@ -162,6 +162,45 @@ def test_partial_and_combine_checks():
     assert st == L.FA_ERR_INVALID_ARG
 
 
+def test_partial_and_combine_alignment():
+    """fa_combine moves 16 B per lane through o_part / o; lse is read per element (float,
+    {lse, e} float pairs for scaled fp16, double for fp64): misaligned buffers are refused."""
+    lib = L.lib()
+    a16, a8, a4 = ctypes.c_void_p(0x10000), ctypes.c_void_p(0x10008), ctypes.c_void_p(0x10004)
+    S = L.FA_DTYPE_FP16_SCALED
+    for o_part, o in ((a8, a16), (a16, a4)):
+        st = lib.fa_combine(o_part, a16, o, 2, 1, 1, 64, 64, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
+        assert st == L.FA_ERR_INVALID_ARG and b"16-byte" in lib.fa_last_error()
+    st = lib.fa_combine(a16, a4, a16, 2, 1, 1, 64, 64, L.FA_DTYPE_BF16, S, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"lse" in lib.fa_last_error()
+    st = lib.fa_combine(a16, ctypes.c_void_p(0x10002), a16, 2, 1, 1, 64, 64, L.FA_DTYPE_BF16,
+                        L.FA_DTYPE_FP32, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"lse" in lib.fa_last_error()
+    st = lib.fa_fwd_partial(a16, a16, a16, a16, a4, 1, 1, 64, 64, 64, 64, L.FA_DTYPE_BF16, S, NULL)
+    assert st == L.FA_ERR_INVALID_ARG and b"lse" in lib.fa_last_error()
+    st = lib.fa_fwd_partial(a16, a16, a16, a16, a4, 1, 1, 64, 64, 64, 64, L.FA_DTYPE_FP64, L.FA_DTYPE_FP64, NULL)
+    assert st == L.FA_ERR_INVALID_ARG
+
+
+def test_split_grid_bound():
+    """One workgroup per (query tile, split, b*h): a grid past 2^31-1 is refused with
+    FA_ERR_UNSUPPORTED (never truncated to 32 bits), before any launch."""
+    lib = L.lib()
+    nbytes, ns = ctypes.c_size_t(), ctypes.c_int()
+    # B*H = 2^16, L = 2^20: 8192 query tiles x 16384 one-tile splits x 65536 heads
+    st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                      ctypes.byref(nbytes), ctypes.byref(ns))
+    assert st == L.FA_ERR_UNSUPPORTED and b"2^31-1" in lib.fa_last_error()
+    fake = ctypes.c_void_p(0x10000)
+    st = lib.fa_fwd_v2(fake, fake, fake, fake, 256, 256, 1 << 20, 64, 32, 32, 1, fake, 1 << 40,
+                       L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED
+    # the same shape with long splits fits: 8192 x 1 x 65536 < 2^31
+    st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1 << 14, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                      ctypes.byref(nbytes), ctypes.byref(ns))
+    assert st == 0 and ns.value == 1
+
+
 def test_python_check_raises_typed_errors():
     lib = L.lib()
     with pytest.raises(L.FaArgumentError) as ei:

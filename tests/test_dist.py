@@ -104,3 +104,48 @@ def test_shard_bounds():
     assert [shard_bounds(16384, 8, r) for r in (0, 7)] == [(0, 2048), (14336, 16384)]
     with pytest.raises(ValueError):
         shard_bounds(100, 8, 0)
+
+
+def _surface_worker(rank, world, port, result_path):
+    """The public surface flash_attention_v2(Q, K, V, world_size=W) (v2.py): every rank passes
+    the full Q, K, V and gets the full O; kernels replaced by the oracle as above."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from exploring_flash_attention_amd import dist as fdist
+    from exploring_flash_attention_amd import v2
+    fdist._partial_fn = _oracle_partial
+    fdist._combine_fn = _oracle_combine
+    fdist._partial_chunk_fn = _oracle_partial_chunk
+    seen = []
+    orig = fdist.splitkv_attention
+
+    def spy(*a, **kw):
+        seen.append(kw.get("partial_dtype"))
+        return orig(*a, **kw)
+    fdist.splitkv_attention = spy
+    g = torch.Generator().manual_seed(5)
+    B, H, L, d = 2, 2, 96, 32
+    errs = []
+    for dtype in (torch.float64, torch.float32):
+        q, k, v = (torch.randn(B, H, L, d, generator=g, dtype=dtype) for _ in range(3))
+        o = v2.flash_attention_v2(q, k, v, world_size=world)
+        ref = attention_fp64(q.double().numpy(), k.double().numpy(), v.double().numpy())
+        assert tuple(o.shape) == (B, H, L, d)
+        errs.append(float(np.abs(o.double().numpy() - ref).max()))
+    with open(f"{result_path}.{rank}", "w") as f:
+        f.write(f"{errs[0]} {errs[1]} {seen[0]} {seen[1]}")
+    dist.destroy_process_group()
+
+
+def test_v2_surface_world_size_2(tmp_path):
+    """flash_attention_v2(..., world_size=2) over gloo: full O on every rank, and the
+    partial format left to splitkv_attention's default (fp64 for fp64 inputs, per-row scaled
+    fp16 otherwise) -- the same exchange format as every other multi-GPU entry point."""
+    port = _free_port()
+    path = str(tmp_path / "res")
+    mp.start_processes(_surface_worker, args=(2, port, path), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        e64, e32, p64, p32 = open(f"{path}.{r}").read().split(" ")
+        assert float(e64) < 1e-6 and float(e32) < 4 * 2.0 ** -11
+        assert p64 == "None" and p32 == "None"

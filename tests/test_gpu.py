@@ -576,3 +576,30 @@ def test_w64_kernel(gpu, dtype):
         q, k, v = _inputs(B, H, L, 128, dtype, seed=40 + i)
         out = ops.attention_v1_w64(q.to(gpu), k.to(gpu), v.to(gpu))
         _gate(out, _ref(q, k, v), dtype)
+
+
+def test_scaled_partials_near_bf16_max(gpu):
+    """Rows whose output approaches bf16's maximum (|O| ~ 2e38, partial exponent e = 128):
+    both combines (in-kernel and fa_combine) weight the splits by 2^(e - E) and apply 2^E
+    after the division, so 2^e itself never overflows fp32.  Peaked rows (q = k: each query's
+    own key dominates), so that O ~ one V row and the unnormalised accumulator stays finite."""
+    from exploring_flash_attention_amd import ops
+    B, H, L, d = 1, 2, 256, 64
+    g = torch.Generator().manual_seed(61)
+    k = torch.randn(B, H, L, d, generator=g) * 4
+    v = (torch.rand(B, H, L, d, generator=g) * 2 - 1) * 3e38
+    q, k, v = (x.to(torch.bfloat16) for x in (k.clone(), k, v))
+    ref = _ref(q, k, v)
+    assert np.abs(ref).max() > 2 ** 127  # rows with exponent 128
+    qg, kg, vg = q.to(gpu), k.to(gpu), v.to(gpu)
+    W = 4
+    parts = [ops.attention_partial(qg, kg[:, :, j * L // W:(j + 1) * L // W].contiguous(),
+                                   vg[:, :, j * L // W:(j + 1) * L // W].contiguous(),
+                                   partial_dtype=ops.PARTIAL_FP16_SCALED) for j in range(W)]
+    sharded = ops.combine(torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]), B, H,
+                          torch.bfloat16)
+    for name, o in (("v2_fused", ops.attention_v2(qg, kg, vg, 1, partial_dtype=ops.PARTIAL_FP16_SCALED)),
+                    ("sharded", sharded), ("v1", ops.attention_v1(qg, kg, vg))):
+        o = o.double().cpu().numpy()
+        assert np.isfinite(o).all(), name
+        assert np.abs(o - ref).max() <= 1e-2 * 3e38, name
