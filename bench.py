@@ -349,26 +349,37 @@ def main():
         # before the headline, so the headline's window also finds the clock settled.
         # (C3's tiled-d form is the same launch as the headline: fa_fwd_v1_tiled_d validates
         # the d tiles and runs the fused kernel)
-        for name, c, fn in (("c2_fused", "c2", "v1"), ("c4_splitkv", "c4", "v2"),
-                            ("c4_splitkv_auto", "c4", "v2auto")):
+        # C4 (KV_TILES_PER_BLOCK = 4: 16 key blocks of 256 keys per query tile) as scheduled
+        # by the library (blocks of a query tile grouped on workgroups, fa_fwd_v2_split_plan),
+        # with the group fixed at 4 and at 1 (FA_SPLIT_GROUP: every block its own workgroup
+        # and HBM partial), and the occupancy-chosen split
+        for name, c, fn, grp in (("c2_fused", "c2", "v1", None), ("c4_splitkv", "c4", "v2", None),
+                                 ("c4_splitkv_4_blocks_per_wg", "c4", "v2", "4"),
+                                 ("c4_splitkv_1_block_per_wg", "c4", "v2", "1"),
+                                 ("c4_splitkv_auto", "c4", "v2auto", None)):
             cc = CONFIGS[c]
             qq, kk, vv = _make_inputs(torch, dev, cc["B"], cc["H"], cc["L"], cc["d"], seed=7)
+            if grp is not None:
+                os.environ["FA_SPLIT_GROUP"] = grp
             if fn == "v1":
                 def st():
                     ops.attention_v1(qq, kk, vv)
             else:  # KV_TILES_PER_BLOCK = 4 as in C4, or the occupancy-chosen split
                 kvt = 4 if fn == "v2" else "auto"
                 nb, nsp = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
+                plan = ops.v2_split_plan(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
                 wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
 
                 def st():
                     ops.attention_v2(qq, kk, vv, kvt, workspace=wsx)
             n = 50
             _, ems = time_step(torch, st, n, 20, barrier)
+            os.environ.pop("FA_SPLIT_GROUP", None)
             f = flops(cc["B"], cc["H"], cc["L"], cc["d"])
             extra[name] = {"ms": round(ems / n, 4), "tflops": round(f / (ems / n * 1e-3) / 1e12, 1)}
             if fn.startswith("v2"):
-                extra[name]["splits"] = nsp
+                extra[name].update(key_blocks=plan[0], blocks_per_workgroup=plan[1], partials_per_tile=plan[2],
+                                   workspace_bytes=nb)
             del qq, kk, vv
         torch.cuda.empty_cache()
 

@@ -28,6 +28,7 @@ FA_KV_TILES_AUTO = -1  # kv_tiles_per_block: split chosen from the device's occu
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _I = ctypes.c_int
+_PI = ctypes.POINTER(ctypes.c_int)
 
 # name -> (restype, argtypes); must cover every function in include/fa_mi355x.h
 SIGNATURES = {
@@ -40,6 +41,7 @@ SIGNATURES = {
     "fa_fwd_v1_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, ctypes.c_double, _I, _P]),
     "fa_fwd_v1_w64": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
     "fa_fwd_v1_tiled_d": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P]),
+    "fa_fwd_v2_split_plan": (_I, [_I64, _I64, _I64, _I64, _I, _I, _PI, _PI, _PI]),
     "fa_fwd_v2_workspace_size": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I,
                                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_I)]),
     "fa_fwd_v2": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,

@@ -6,6 +6,7 @@
 //   0 < d_tile_qk, d_tile_v <= d   flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327
 //   kv_tiles_per_block > 0         flash_attention_v2/CUDA/flash_attention_v2.h:447
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -214,10 +215,43 @@ int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
     return (int)((ntiles + ns - 1) / ns);
 }
 
-int splits_for(int64_t L, int64_t d, int kvtpb, int* kv_per_split, fa::Elem e) {
+// Split-KV scheduling.  The reference splits each head's keys into blocks of
+// kv_tiles_per_block tiles, one partial per block, and reduces the partials
+// (flash_attention_v2/CUDA/flash_attention_v2.h:243, :356).  Here consecutive blocks of a
+// query tile are grouped onto one workgroup: the blocks of a group are combined on chip (the
+// online softmax carried across them -- algebraically the reduction's formula, split after
+// split), the groups' partials through the workspace and the in-kernel reduction.  As many
+// blocks go to one group as still leave >= 4 workgroups per resident slot, so a problem whose
+// query tiles already fill the GPU moves no partials through HBM at all, and a short-batch
+// long-sequence one gets one workgroup per block.  FA_SPLIT_GROUP=<n> (environment) fixes
+// the group size for measurements (1 = one workgroup and one HBM partial per block).
+struct SplitPlan {
+    int units;       // the reference's key blocks: ceil(L / (kv_tiles_per_block * bk))
+    int group;       // blocks per workgroup
+    int launched;    // partial workgroups per query tile: ceil(units / group)
+    int kv_per_wg;   // keys per workgroup (group * block keys, at most L)
+};
+SplitPlan plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, fa::Elem e) {
+    SplitPlan p{};
     const int64_t keys = (int64_t)kvtpb * keys_per_tile(e, d);
-    *kv_per_split = (int)(keys < L ? keys : L);
-    return (int)((L + keys - 1) / keys);
+    p.units = (int)((L + keys - 1) / keys);
+    const int64_t items = BH * ((L + rows_per_block(e) - 1) / rows_per_block(e));
+    p.group = 1;
+    if (const char* env = std::getenv("FA_SPLIT_GROUP")) {
+        const int g = std::atoi(env);
+        if (g >= 1) p.group = g < p.units ? g : p.units;
+    } else {
+        const int64_t want = 4 * (int64_t)resident_workgroups(d);
+        for (int g = p.units; g > 1; --g)
+            if (items * ((p.units + g - 1) / g) >= want) {
+                p.group = g;
+                break;
+            }
+    }
+    p.launched = (p.units + p.group - 1) / p.group;
+    const int64_t kw = keys * p.group;
+    p.kv_per_wg = (int)(kw < L ? kw : L);
+    return p;
 }
 
 }  // namespace
@@ -307,17 +341,32 @@ int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_
     if (kv_tiles_per_block <= 0)
         return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
-    int kvps;
-    const int ns = splits_for(L, d, kv_tiles_per_block, &kvps, e);
-    // one workgroup per (query tile, split, b*h): the grid and the kernel's block index are
-    // 32-bit (dim3, xcd_remap), so a grid past 2^31-1 is refused instead of truncated
+    const SplitPlan sp = plan_splits(B * H, L, d, kv_tiles_per_block, e);
+    const int ns = sp.launched;
+    // one workgroup per (query tile, split group, b*h): the grid and the kernel's block index
+    // are 32-bit (dim3, xcd_remap), so a grid past 2^31-1 is refused instead of truncated
     const int64_t nqt = (L + rows_per_block(e) - 1) / rows_per_block(e);
     if (B * H * nqt > (int64_t)0x7fffffff / ns)
         return fail(FA_ERR_UNSUPPORTED, "split-KV grid of %lld x %d workgroups exceeds 2^31-1 "
                     "(raise kv_tiles_per_block)", (long long)(B * H * nqt), ns);
-    const V2Layout w = v2_layout(B * H, L, d, ns, pe);
-    *bytes = w.total;
-    if (num_splits) *num_splits = ns;
+    // one partial workgroup per query tile: the FA-v1 kernel, no workspace needed
+    *bytes = ns == 1 ? 256 : v2_layout(B * H, L, d, ns, pe).total;
+    if (num_splits) *num_splits = sp.units;
+    return ok();
+}
+
+int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block, int dtype,
+                         int* key_blocks, int* blocks_per_workgroup, int* partials_per_tile) {
+    fa::Elem e;
+    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_dtype(dtype, &e)) return st;
+    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
+    if (kv_tiles_per_block <= 0)
+        return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
+    const SplitPlan p = plan_splits(B * H, L, d, kv_tiles_per_block, e);
+    if (key_blocks) *key_blocks = p.units;
+    if (blocks_per_workgroup) *blocks_per_workgroup = p.group;
+    if (partials_per_tile) *partials_per_tile = p.launched;
     return ok();
 }
 
@@ -347,7 +396,7 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     if (kv_tiles_per_block == FA_KV_TILES_AUTO && check_dtype(dtype, &e) == FA_OK)
         kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
     if (int st = fa_fwd_v2_workspace_size(B, H, L, d, kv_tiles_per_block, dtype, partial_dtype,
-                                          &need, &ns))
+                                          &need, nullptr))
         return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     if (int st = check_d_tiles(d, d_tile_qk, d_tile_v)) return st;
@@ -359,18 +408,18 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     if ((uintptr_t)workspace & 255) return fail(FA_ERR_WORKSPACE, "workspace must be 256-byte aligned");
 
     const int64_t BH = B * H;
+    ns = plan_splits(BH, L, d, kv_tiles_per_block, e).launched;
     fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
     if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
-    if (ns == 1) {  // one split: nothing to combine
+    if (ns == 1) {  // one partial workgroup per query tile: nothing to combine
         if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
             return hip_fail(he, "fa_fwd_v2 launch");
         return ok();
     }
     const V2Layout w = v2_layout(BH, L, d, ns, pe);
-    int kvps;
-    a.nsplit = splits_for(L, d, kv_tiles_per_block, &kvps, e);
-    a.kv_per_split = kvps;
+    a.nsplit = ns;
+    a.kv_per_split = plan_splits(BH, L, d, kv_tiles_per_block, e).kv_per_wg;
     if (e == fa::Elem::F64) {  // fp64: the reference's two kernels (partial, then reduction)
         a.o = workspace;
         a.lse64 = (double*)((char*)workspace + w.lse_off);

@@ -214,8 +214,9 @@ def _kvtpb(kv_tiles_per_block):
 
 def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
                        partial_dtype=None):
-    """(bytes, num_splits) of the split-KV workspace (partials fp32 unless partial_dtype;
-    fp64 for fp64 inputs)."""
+    """(bytes, num_splits) of the split-KV workspace: num_splits = the reference's key blocks;
+    the bytes cover the partials actually combined through the workspace (v2_split_plan) in
+    partial_dtype (per-row scaled fp16 by default; fp64 for fp64 inputs)."""
     pd = _default_pdtype(dtype, partial_dtype, fused=True)
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
     nbytes = ctypes.c_size_t()
@@ -224,6 +225,17 @@ def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
     check(lib().fa_fwd_v2_workspace_size(B, H, L, d, int(kv_tiles_per_block), _DTYPES[dtype],
                                          _PDTYPES[pd], ctypes.byref(nbytes), ctypes.byref(ns)))
     return nbytes.value, ns.value
+
+
+def v2_split_plan(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16):
+    """(key_blocks, blocks_per_workgroup, partials_per_tile) of fa_fwd_v2's schedule: the
+    reference's key blocks of kv_tiles_per_block tiles, how many consecutive blocks one
+    workgroup combines on chip, and how many partial workgroups per query tile are combined
+    through the workspace."""
+    kb, g, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib().fa_fwd_v2_split_plan(B, H, L, kernel_head_dim(d), int(_kvtpb(kv_tiles_per_block)), _DTYPES[dtype],
+                                     ctypes.byref(kb), ctypes.byref(g), ctypes.byref(p)))
+    return kb.value, g.value, p.value
 
 
 def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, partial_dtype=None,

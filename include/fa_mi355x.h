@@ -134,18 +134,29 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o,
 int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o,
                   int64_t B, int64_t H, int64_t L, int64_t d, int dtype, void* stream);
 
-/* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split is
- * kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
- * FA_DTYPE_FP32, the input dtype or FA_DTYPE_FP16_SCALED.  *num_splits (may be NULL) receives the split count. */
+/* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split (the reference's key
+ * block) is kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
+ * FA_DTYPE_FP32, the input dtype or FA_DTYPE_FP16_SCALED.  *num_splits (may be NULL)
+ * receives the number of key blocks.  The size covers the partials fa_fwd_v2 actually moves
+ * through the workspace (fa_fwd_v2_split_plan); it depends on the device's occupancy. */
 int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d,
                              int kv_tiles_per_block, int dtype, int partial_dtype,
                              size_t* bytes, int* num_splits);
 
-/* FA-v2 split-KV forward: one workgroup per (q-tile, split, b*h) computes its split's
- * normalised partial O and log-sum-exp into the workspace; the last workgroup of each
- * q-tile to finish combines the splits with fa_combine's formula and writes O (the
- * reduction kernel's maths without its separate pass over HBM).  One split: the plain
- * FA-v1 kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
+/* How fa_fwd_v2 schedules the key blocks of a query tile: *key_blocks = ceil(L / (kv_tiles_per_block
+ * * bk)) (the reference's partials), *blocks_per_workgroup consecutive blocks per workgroup
+ * (combined on chip: the online softmax carried across them), *partials_per_tile partial
+ * workgroups per query tile (combined through the workspace).  Blocks are grouped as long as
+ * >= 4 workgroups per resident slot remain; FA_SPLIT_GROUP=<n> in the environment fixes the
+ * group size (1: one workgroup and one HBM partial per key block).  Any pointer may be NULL. */
+int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block,
+                         int dtype, int* key_blocks, int* blocks_per_workgroup, int* partials_per_tile);
+
+/* FA-v2 split-KV forward: one workgroup per (q-tile, group of key blocks, b*h) computes its
+ * keys' normalised partial O and log-sum-exp into the workspace; the last workgroup of each
+ * q-tile to finish combines the partials with fa_combine's formula and writes O (the
+ * reduction kernel's maths without its separate pass over HBM).  One partial workgroup per
+ * q-tile (fa_fwd_v2_split_plan): the plain FA-v1 kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
  * 256-byte aligned, contents need not be initialised (a hipMemsetAsync of its counters
  * precedes the launch on `stream`).  d_tile_qk / d_tile_v as for fa_fwd_v1_tiled_d. */
 int fa_fwd_v2(const void* q, const void* k, const void* v, void* o,

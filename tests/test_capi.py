@@ -118,14 +118,34 @@ def test_kernel_head_dim_padding_map():
 def test_workspace_size_and_v2_checks():
     lib = L.lib()
     nbytes, ns = ctypes.c_size_t(), ctypes.c_int()
-    # C4: B32 H8 L4096 d128, KVTPB=4 -> 256-key splits -> 16 splits
+    # C4: B32 H8 L4096 d128, KVTPB=4 -> 256-key blocks -> 16 blocks; the 8192 query tiles fill
+    # the device (no device here: the MI355X's 256 CUs assumed), so all 16 blocks of a tile go
+    # to one workgroup and no partial crosses HBM
     assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, L.FA_DTYPE_BF16,
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+    assert ns.value == 16 and nbytes.value == 256
+    kb, g, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
+                                    ctypes.byref(p)) == 0
+    assert (kb.value, g.value, p.value) == (16, 16, 1)
+    # FA_SPLIT_GROUP=1: one workgroup and one HBM partial per key block (the reference's layout)
+    os.environ["FA_SPLIT_GROUP"] = "1"
+    try:
+        assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, L.FA_DTYPE_BF16,
+                                            ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+        assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                        ctypes.byref(p)) == 0
+    finally:
+        del os.environ["FA_SPLIT_GROUP"]
+    assert (g.value, p.value) == (1, 16)
     rows = 16 * 32 * 8 * 4096
-    assert ns.value == 16
     # partial O + lse (fragment order, 128-row tiles: 4096 = 32 x 128) + one counter per tile
     assert nbytes.value == rows * 128 * 2 + rows * 4 + 32 * 8 * 32 * 4
     assert nbytes.value > 2 ** 32  # 64-bit sizes (the reference overflows int32 here)
+    # a short batch of long sequences: one workgroup per key block
+    assert lib.fa_fwd_v2_split_plan(1, 1, 8192, 128, 4, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
+                                    ctypes.byref(p)) == 0
+    assert (kb.value, g.value, p.value) == (32, 1, 32)
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
     assert ns.value == 2
@@ -187,18 +207,27 @@ def test_split_grid_bound():
     FA_ERR_UNSUPPORTED (never truncated to 32 bits), before any launch."""
     lib = L.lib()
     nbytes, ns = ctypes.c_size_t(), ctypes.c_int()
-    # B*H = 2^16, L = 2^20: 8192 query tiles x 16384 one-tile splits x 65536 heads
+    # B*H = 2^16, L = 2^20, one workgroup per key block (FA_SPLIT_GROUP=1):
+    # 8192 query tiles x 16384 one-tile splits x 65536 heads
+    os.environ["FA_SPLIT_GROUP"] = "1"
+    try:
+        st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                          ctypes.byref(nbytes), ctypes.byref(ns))
+        assert st == L.FA_ERR_UNSUPPORTED and b"2^31-1" in lib.fa_last_error()
+        fake = ctypes.c_void_p(0x10000)
+        st = lib.fa_fwd_v2(fake, fake, fake, fake, 256, 256, 1 << 20, 64, 32, 32, 1, fake, 1 << 40,
+                           L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
+        assert st == L.FA_ERR_UNSUPPORTED
+        # the same shape with long splits fits: 8192 x 1 x 65536 < 2^31
+        st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1 << 14, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                          ctypes.byref(nbytes), ctypes.byref(ns))
+        assert st == 0 and ns.value == 1
+    finally:
+        del os.environ["FA_SPLIT_GROUP"]
+    # scheduled normally, the blocks of a query tile share workgroups and the grid fits
     st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
                                       ctypes.byref(nbytes), ctypes.byref(ns))
-    assert st == L.FA_ERR_UNSUPPORTED and b"2^31-1" in lib.fa_last_error()
-    fake = ctypes.c_void_p(0x10000)
-    st = lib.fa_fwd_v2(fake, fake, fake, fake, 256, 256, 1 << 20, 64, 32, 32, 1, fake, 1 << 40,
-                       L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
-    assert st == L.FA_ERR_UNSUPPORTED
-    # the same shape with long splits fits: 8192 x 1 x 65536 < 2^31
-    st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1 << 14, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
-                                      ctypes.byref(nbytes), ctypes.byref(ns))
-    assert st == 0 and ns.value == 1
+    assert st == 0 and ns.value == 16384
 
 
 def test_python_check_raises_typed_errors():

@@ -57,13 +57,20 @@ def test_fullsize_v1_and_tiled_d(gpu, d):
     _check_sampled(ops.attention_tiled_d(q, k, v, 32, 32), q, k, v)
 
 
-@pytest.mark.parametrize("kvt", [4, "auto"], ids=["kvtpb4", "auto"])
-def test_fullsize_c4_splitkv(gpu, kvt):
+@pytest.mark.parametrize("kvt,group", [(4, None), (4, "1"), (4, "4"), ("auto", None)],
+                         ids=["kvtpb4", "kvtpb4-one-wg-per-block", "kvtpb4-4-per-wg", "auto"])
+def test_fullsize_c4_splitkv(gpu, kvt, group, monkeypatch):
+    """C4 as scheduled (the 16 key blocks of a query tile on one workgroup), and with
+    FA_SPLIT_GROUP fixing 1 or 4 blocks per workgroup: 16 / 4 partials per query tile
+    through the workspace and the in-kernel combine (8192 query tiles)."""
     from exploring_flash_attention_amd import ops
+    if group is not None:
+        monkeypatch.setenv("FA_SPLIT_GROUP", group)
     q, k, v = _device_inputs(4096, 128, seed=4)
     nbytes, ns = ops.v2_workspace_bytes(B, H, 4096, 128, kvt)
+    blocks, per_wg, partials = ops.v2_split_plan(B, H, 4096, 128, kvt)
     if kvt == 4:
-        assert ns == 16
+        assert ns == blocks == 16 and partials == 16 // int(group or 16)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
     o1 = ops.attention_v2(q, k, v, kvt, workspace=ws)
     o2 = ops.attention_v2(q, k, v, kvt, workspace=ws)
