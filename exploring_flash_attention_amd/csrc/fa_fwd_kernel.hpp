@@ -69,6 +69,9 @@
 #ifndef FA_ABL_NODMAWAIT
 #define FA_ABL_NODMAWAIT 0
 #endif
+#ifndef FA_ABL_NOBAR
+#define FA_ABL_NOBAR 0
+#endif
 #ifndef FA_ABL_NOEXP
 #define FA_ABL_NOEXP 0
 #endif
@@ -571,7 +574,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             });
         }
 #endif
-#if FA_ABL_NODMAWAIT
+#if FA_ABL_NOBAR
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#elif FA_ABL_NODMAWAIT
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
 #else
