@@ -1,10 +1,12 @@
 #!/bin/bash
 # PMC passes (one counter group per pass, --kernel-trace only, never with sys/runtime trace)
-# over scripts/run_kernel.py.  Usage: bash scripts/profile_pmc.sh [config] ; output gpurun_out/pmc_<cfg>/
+# over scripts/run_kernel.py.  Usage: bash scripts/profile_pmc.sh [config] [name] ; output
+# gpurun_out/pmc_<name>/ (name defaults to the config; environment, e.g. FA_SPLIT_GROUP, passes through)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 CFG=${1:-c3}
-OUT=gpurun_out/pmc_$CFG
+NAME=${2:-$CFG}
+OUT=gpurun_out/pmc_$NAME
 mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true

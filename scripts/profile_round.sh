@@ -11,10 +11,14 @@ timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --outpu
     python bench.py --no-cpu-baseline --no-extra > $OUT/prof_bench.json 2> $OUT/prof.log; rc=$?
 echo "kernel-trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
-for cfg in c3 c2; do
+cp profiles/hbm_traffic.json $OUT/hbm_traffic.json 2>/dev/null
+for cfg in c3 c2 c4; do
   bash scripts/profile_pmc.sh $cfg || exit $?
   python scripts/traffic.py gpurun_out/pmc_$cfg $cfg $OUT/hbm_traffic.json > /dev/null || exit $?
 done
+# C4 with 4 key blocks per workgroup (4 partials per query tile through the workspace)
+FA_SPLIT_GROUP=4 bash scripts/profile_pmc.sh c4 c4g4 || exit $?
+python scripts/traffic.py gpurun_out/pmc_c4g4 c4g4 $OUT/hbm_traffic.json > /dev/null || exit $?
 cat $OUT/kernel_stats.csv | head -3
 python - <<'PY'
 import json
