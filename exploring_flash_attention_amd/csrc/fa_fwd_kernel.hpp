@@ -121,10 +121,14 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 #ifndef FA_STAMPS
 #define FA_STAMPS 0
 #endif
-#if FA_STAMPS
+#if FA_STAMPS && defined(FA_FWD_MAIN_TU)
+// (only the contiguous launches of fa_fwd.hip are stamped: a device symbol shared between
+// translation units would need relocatable device code)
 #define FA_MAX_STAMP_WG 65536
-#ifdef FA_FWD_MAIN_TU
 __device__ unsigned long long g_fa_stamps[FA_MAX_STAMP_WG * 16];
+extern "C" int fa_debug_stamps(void* dst, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fa_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
 #define FA_STAMP_V(i, v)                                                                       \
     do {                                                                                       \
         if (tid == 0 && blockIdx.x < FA_MAX_STAMP_WG)                                          \
@@ -132,12 +136,6 @@ __device__ unsigned long long g_fa_stamps[FA_MAX_STAMP_WG * 16];
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     \
     } while (0)
 #define FA_STAMP(i) FA_STAMP_V(i, __builtin_amdgcn_s_memtime())
-extern "C" int fa_debug_stamps(void* dst, size_t bytes) {
-    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fa_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-#else
-extern __device__ unsigned long long g_fa_stamps[FA_MAX_STAMP_WG * 16];
-#endif
 #else
 #define FA_STAMP_V(i, v) \
     do {                 \
