@@ -48,6 +48,17 @@
 #ifndef FA_MFMA_ROWSUM_MAXD
 #define FA_MFMA_ROWSUM_MAXD 0
 #endif
+// FA_ROWSUM16_MASK (head-dim bits): the softmax denominator on v_mfma_f32_16x16x32 instead of
+// VALU adds: A = a 0/1 pattern, B = each packed P^T fragment as it is, so one MFMA per
+// 16-key fragment sums both key halves of 16 query rows into 4 accumulator registers
+// (lane l ends up holding the sum of query row (l & 15) + 16 * (l >> 5)); sums the same
+// 16-bit-rounded P the numerator uses
+// (final mode, no key tail, contiguous tensors only; A/B at C2: +3.5 %, same error.  Those
+// d = 32 kernels are held to 128 registers -- four waves per SIMD -- which costs them a few
+// spills after the KV loop; the other d = 32 instantiations would spill inside it)
+#ifndef FA_ROWSUM16_MASK
+#define FA_ROWSUM16_MASK 1
+#endif
 #ifndef FA_DMA_LATE
 #define FA_DMA_LATE 1
 #endif
@@ -95,6 +106,13 @@
 #define FA_NOTAIL_MASK 0xD
 #endif
 constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
+constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
+    return (FA_ROWSUM16_MASK & d_bit(d)) != 0 && mode == 0 && !tail && !strided;
+}
+// launch bound (waves per SIMD) of an instantiation: the RS16 kernels are sized for four
+constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
+    return rs16_on(d, mode, tail, strided) && d <= 32 ? 4 : fa::waves_per_simd(d);
+}
 #ifndef FA_RSRC32
 #define FA_RSRC32 1
 #endif
@@ -108,6 +126,13 @@ constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8
 // initial value, so the exponent needs no per-score FMA
 #ifndef FA_QSCALE_MASK
 #define FA_QSCALE_MASK 0  // off: +2-4 % but peaked rows lose accuracy
+#endif
+// FA_QSPLIT_MASK (head-dim bits; 16-bit brain-float inputs only): QSCALE with c*Q split into
+// two bf16 terms (hi + lo: ~16 significant bits, so peaked rows keep their accuracy) and -m
+// entered by one more MFMA per 32-key block (A = ones in k = 0..2, B = -m as three bf16
+// terms) instead of a splat of -m into the accumulators
+#ifndef FA_QSPLIT_MASK
+#define FA_QSPLIT_MASK 0
 #endif
 #ifndef FA_PK_MAXD
 #define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
@@ -152,7 +177,7 @@ namespace fa {
 // (d contiguous, K and V sharing strides), e.g. [B, L, H, d] tensors viewed as [B, H, L, d];
 // false (contiguous [B, H, L, d]) folds every stride to a constant.
 template <typename T, typename PT, int D, int MODE, bool TAIL, bool STRIDED = false>
-__global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void fa_fwd_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     constexpr int RB = kRB;                   // 32-row query blocks per wave
@@ -167,8 +192,10 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     // bounded by 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows
     // (the dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
     constexpr float kThr = 4.f;
-    constexpr bool QSCALE = (FA_QSCALE_MASK & d_bit(D)) != 0;
+    constexpr bool QSPLIT = (FA_QSPLIT_MASK & d_bit(D)) != 0 && std::is_same_v<T, __bf16>;
+    constexpr bool QSCALE = (FA_QSCALE_MASK & d_bit(D)) != 0 || QSPLIT;
     constexpr bool FA_MFMA_ROWSUM = D <= FA_MFMA_ROWSUM_MAXD;
+    constexpr bool RS16 = rs16_on(D, MODE, TAIL, STRIDED) && !FA_MFMA_ROWSUM;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: K ring (2 slots) then V ring (2 slots), one [kBK][D] tile image per slot.
@@ -285,6 +312,16 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
     f32x16 lsum[RB];     // FA_MFMA_ROWSUM: every register = the row sum of the lane's query
 #pragma unroll
     for (int r = 0; r < RB; ++r) lsum[r] = f32x16{};
+    f32x4 ls16[RB];  // RS16: row sum of query (lane & 15) + 16 * (lane >> 5), in every register
+#pragma unroll
+    for (int r = 0; r < RB; ++r) ls16[r] = f32x4{};
+    // A of the RS16 MFMA: output rows 0-7 sum lane groups 0 and 2 (query n, both key halves),
+    // rows 8-15 groups 1 and 3 (query n + 16)
+    v8 sel16;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sel16[j] = static_cast<T>(((lane & 15) < 8) == (((lane >> 4) & 1) == 0) ? 1.f : 0.f);
+    const int rs16_src = ((lane & 31) < 16 ? (lane & 31) : (lane & 31) + 16) * 4;  // holder of own row
+    const int rs16_row = ((lane & 15) + 16 * (lane >> 5)) * 4;                      // row held here
     v8 ones;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ones[j] = static_cast<T>(1.0f);
@@ -294,6 +331,29 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         l[r] = 0.f;
     }
     const float c = a.scale_log2;
+    // QSPLIT: the low bf16 term of c*Q, and the bias MFMA's operands (-m as hi + mid + lo)
+    v8 qlo[RB][QSPLIT ? NKS : 1];
+    v8 bias_a, bias_b[RB];
+    auto set_bias = [&](int r) {
+        const float nm = -m[r];
+        const T h = static_cast<T>(nm);
+        const float r1 = nm - static_cast<float>(h);
+        const T mid = static_cast<T>(r1);
+        const T lo = static_cast<T>(r1 - static_cast<float>(mid));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bias_b[r][j] = static_cast<T>(0.f);
+        if (hf == 0) {
+            bias_b[r][0] = h;
+            bias_b[r][1] = mid;
+            bias_b[r][2] = lo;
+        }
+    };
+    if constexpr (QSPLIT) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bias_a[j] = static_cast<T>(hf == 0 && j < 3 ? 1.f : 0.f);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) set_bias(r);
+    }
 
     // S^T[key][q] = K . Q^T for one tile (two 32-key blocks), every K fragment feeding the
     // RB row blocks.  Fragments are read in groups of two k-steps, one group ahead.
@@ -311,7 +371,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
         for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int b2 = 0; b2 < NKB; ++b2) {
-                if constexpr (QSCALE) {
+                if constexpr (QSPLIT) {
+                    s[r][b2] = f32x16{};
+                } else if constexpr (QSCALE) {
                     const float nm = -m[r];
                     const double nm2 = __builtin_bit_cast(double, f32x2{nm, nm});
                     typedef double d8 __attribute__((ext_vector_type(8)));
@@ -336,12 +398,35 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                         s[r][b2][j] += (float)qf[r][g * G + j][0];
 #else
                         s[r][b2] = M::mma(kf[g & 1][b2][j], qf[r][g * G + j], s[r][b2]);
+                        if constexpr (QSPLIT) s[r][b2] = M::mma(kf[g & 1][b2][j], qlo[r][g * G + j], s[r][b2]);
 #endif
                     }
+        }
+        if constexpr (QSPLIT) {
+#pragma unroll
+            for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                for (int r = 0; r < RB; ++r) s[r][b2] = M::mma(bias_a, bias_b[r], s[r][b2]);
         }
     };
     // P = 2^(S*c - m) in place, and its row sum into l
     auto exp_tile = [&](f32x16 (&s)[RB][NKB]) {
+        if constexpr (D <= FA_PK_MAXD && !FA_MFMA_ROWSUM && RS16) {
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const f32x2 c2 = {c, c}, nm2 = {-m[r], -m[r]};
+#pragma unroll
+                for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                    for (int i = 0; i < 16; i += 2) {
+                        f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
+                        if constexpr (!QSCALE) x = __builtin_elementwise_fma(x, c2, nm2);
+                        s[r][b2][i] = __builtin_amdgcn_exp2f(x[0]);
+                        s[r][b2][i + 1] = __builtin_amdgcn_exp2f(x[1]);
+                    }
+            }
+            return;
+        }
         if constexpr (D <= FA_PK_MAXD && !FA_MFMA_ROWSUM) {
             // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU instruction where
             // the MFMA pipe is mostly idle (small d is VALU-bound)
@@ -378,9 +463,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #else
                     s[r][b2][i] = __builtin_amdgcn_exp2f(QSCALE ? s[r][b2][i] : __builtin_fmaf(s[r][b2][i], c, -m[r]));
 #endif
-                    if (!FA_MFMA_ROWSUM) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
+                    if (!FA_MFMA_ROWSUM && !RS16) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
                 }
-            if (!FA_MFMA_ROWSUM) l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
+            if (!FA_MFMA_ROWSUM && !RS16) l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
         }
     };
     // keys past the end of the split (only in the last, partial tile) -> -inf
@@ -474,7 +559,10 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                 const float delta = fmaxf(mx[r], 0.f);
                 const float alpha = __builtin_amdgcn_exp2f(-delta);
                 m[r] += delta;
+                if constexpr (QSPLIT) set_bias(r);
                 l[r] *= alpha;
+                if constexpr (RS16)
+                    ls16[r] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
 #pragma unroll
                 for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
@@ -489,6 +577,8 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                 m[r] = m_new;
                 l[r] *= alpha;
                 if (FA_MFMA_ROWSUM) lsum[r] *= alpha;
+                if constexpr (RS16)
+                    ls16[r] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
 #pragma unroll
                 for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
             }
@@ -541,6 +631,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
                     o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
 #endif
                     if (FA_MFMA_ROWSUM && DB == 0) lsum[r] = M::mma(ones, pb[r][B2][ss], lsum[r]);
+                    if constexpr (RS16 && DB == 0) ls16[r] = M::mma16(sel16, pb[r][B2][ss], ls16[r]);
                 }
             }
             if constexpr (I + 1 < NKB * NDB) {
@@ -601,7 +692,11 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) qf[r][ks][j] = static_cast<T>(static_cast<float>(qf[r][ks][j]) * c);
+                for (int j = 0; j < 8; ++j) {
+                    const float x = static_cast<float>(qf[r][ks][j]) * c;
+                    qf[r][ks][j] = static_cast<T>(x);
+                    if constexpr (QSPLIT) qlo[r][ks][j] = static_cast<T>(x - static_cast<float>(qf[r][ks][j]));
+                }
         }
     }
     __syncthreads();
@@ -615,6 +710,7 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             m[r] = mx[r];
+            if constexpr (QSPLIT) set_bias(r);
 #pragma unroll
             for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
@@ -719,7 +815,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
             const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
-                const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
+                const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0]
+                            : RS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_src, __builtin_bit_cast(int, ls16[r][0])))
+                                   : pair_sum(l[r]);
                 inv[r] = 1.f / l_tot;
                 lse_own[r] = m[r] + __builtin_amdgcn_logf(l_tot);
                 esc_own[r] = 0.f;
@@ -864,7 +962,9 @@ __global__ __launch_bounds__(kThreads, waves_per_simd(D)) void fa_fwd_kernel(Fwd
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         const int64_t q_row = q_row0 + 32 * r;
-        const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0] : pair_sum(l[r]);
+        const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0]
+                            : RS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_src, __builtin_bit_cast(int, ls16[r][0])))
+                                   : pair_sum(l[r]);
         float inv = 1.f / l_tot;
         if (q_row >= a.Lq) continue;
         if constexpr (MODE == kFinal) {
