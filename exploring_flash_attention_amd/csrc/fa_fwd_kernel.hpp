@@ -53,11 +53,12 @@
 // 16-key fragment sums both key halves of 16 query rows into 4 accumulator registers
 // (lane l ends up holding the sum of query row (l & 15) + 16 * (l >> 5)); sums the same
 // 16-bit-rounded P the numerator uses
-// (final mode, no key tail, contiguous tensors only; A/B at C2: +3.5 %, same error.  Those
-// d = 32 kernels are held to 128 registers -- four waves per SIMD -- which costs them a few
-// spills after the KV loop; the other d = 32 instantiations would spill inside it)
+// (final mode, no key tail, contiguous tensors only; A/B: C2 +3.5 %, C3 +1.2 %, L = 2048
+// +1.3 %, errors equal or lower; d = 64 would drop to two waves per SIMD.  The d = 32 kernels
+// are held to 128 registers -- four waves per SIMD -- and, like d = 128, spill a few registers
+// after the KV loop, none inside it; the other instantiations would spill inside it)
 #ifndef FA_ROWSUM16_MASK
-#define FA_ROWSUM16_MASK 1
+#define FA_ROWSUM16_MASK 5
 #endif
 #ifndef FA_DMA_LATE
 #define FA_DMA_LATE 1
