@@ -53,10 +53,11 @@
 // 16-key fragment sums both key halves of 16 query rows into 4 accumulator registers
 // (lane l ends up holding the sum of query row (l & 15) + 16 * (l >> 5)); sums the same
 // 16-bit-rounded P the numerator uses
-// (final mode, no key tail, contiguous tensors only; A/B: C2 +3.5 %, C3 +1.2 %, L = 2048
-// +1.3 %, errors equal or lower; d = 64 would drop to two waves per SIMD.  The d = 32 kernels
-// are held to 128 registers -- four waves per SIMD -- and, like d = 128, spill a few registers
-// after the KV loop, none inside it; the other instantiations would spill inside it)
+// (no key tail, contiguous tensors; at d = 32 the final mode only.  A/B: C2 +3.5 %, C3
+// +1.2 %, L = 2048 +1.3 %, the C5 partial kernel +1.4 %, the fused split 0; errors equal or
+// lower; d = 64 would drop to two waves per SIMD.  The d = 32 final kernel is held to 128
+// registers -- four waves per SIMD -- and, like d = 128, spills a few registers after the KV
+// loop, none inside it; the other d = 32 instantiations would spill inside it)
 #ifndef FA_ROWSUM16_MASK
 #define FA_ROWSUM16_MASK 5
 #endif
@@ -108,7 +109,7 @@
 #endif
 constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
 constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
-    return (FA_ROWSUM16_MASK & d_bit(d)) != 0 && mode == 0 && !tail && !strided;
+    return (FA_ROWSUM16_MASK & d_bit(d)) != 0 && (mode == 0 || d > 32) && !tail && !strided;
 }
 // launch bound (waves per SIMD) of an instantiation: the RS16 kernels are sized for four
 constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--acc", action="store_true", help="also report the error against fp32")
     ap.add_argument("--kvtpb", type=int, default=0, help="time fa_fwd_v2 with this kv_tiles_per_block")
+    ap.add_argument("--partial", action="store_true",
+                    help="time fa_fwd_partial over all keys (scaled fp16 partials: the C5 per-rank kernel)")
     args = ap.parse_args()
     B, H, L, d = CFG[args.config]
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -37,6 +39,8 @@ def main():
         h.fa_fwd_v1.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64] * 4 + [ctypes.c_int, ctypes.c_void_p]
         h.fa_fwd_v2.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_int64] * 4 + [ctypes.c_int] * 3 +
                                 [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+        h.fa_fwd_partial.argtypes = ([ctypes.c_void_p] * 5 + [ctypes.c_int64] * 6 +
+                                     [ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
         h.fa_fwd_v2_workspace_size.argtypes = [ctypes.c_int64] * 4 + [ctypes.c_int] * 3 + [
             ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]
         libs.append(h)
@@ -48,8 +52,17 @@ def main():
         ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
         print(f"v2: kv_tiles_per_block {args.kvtpb}, {ns.value} splits, workspace {nb.value / 1e9:.2f} GB")
 
+    part = None
+    if args.partial:
+        part = [(torch.empty(B, H, L, d, dtype=torch.float16, device="cuda"),
+                 torch.empty(B, H, L, 2, dtype=torch.float32, device="cuda")) for _ in libs]
+
     def run(i):
-        if ws is not None:
+        if part is not None:
+            st = libs[i].fa_fwd_partial(q.data_ptr(), k.data_ptr(), v.data_ptr(), part[i][0].data_ptr(),
+                                        part[i][1].data_ptr(), B, H, L, L, d, L, 1, 4, stream)
+            outs[i] = part[i][0]
+        elif ws is not None:
             st = libs[i].fa_fwd_v2(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d,
                                    min(32, d), min(32, d), args.kvtpb, ws.data_ptr(), ws.numel(), 1, 4, stream)
         else:
