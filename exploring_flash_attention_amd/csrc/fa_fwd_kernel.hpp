@@ -53,13 +53,14 @@
 // 16-key fragment sums both key halves of 16 query rows into 4 accumulator registers
 // (lane l ends up holding the sum of query row (l & 15) + 16 * (l >> 5)); sums the same
 // 16-bit-rounded P the numerator uses
-// (no key tail, contiguous tensors; at d = 32 the final mode only.  A/B: C2 +3.5 %, C3
-// +1.2 %, L = 2048 +1.3 %, the C5 partial kernel +1.4 %, the fused split 0; errors equal or
-// lower; d = 64 would drop to two waves per SIMD.  The d = 32 final kernel is held to 128
-// registers -- four waves per SIMD -- and, like d = 128, spills a few registers after the KV
-// loop, none inside it; the other d = 32 instantiations would spill inside it)
+// (at d = 32 the final no-tail contiguous kernel only; elsewhere every mode, key tails and
+// strided tensors alike, so that a strided view gives the contiguous result bit for bit.  A/B: C2 +3.5 %, C3 +1.2 %,
+// L = 2048 +1.3 %, L = 1000 (key tail) +1.3 %, d = 64 +1.7 %, the C5 partial kernel +1.4 %,
+// the fused split 0; errors equal or lower.  The d = 32 kernel is held to 128 registers and
+// d = 64 to 168 -- four / three waves per SIMD, as without it -- and they and d = 128 spill a
+// few registers after the KV loop, none inside it; the other d = 32 instantiations would)
 #ifndef FA_ROWSUM16_MASK
-#define FA_ROWSUM16_MASK 5
+#define FA_ROWSUM16_MASK 7
 #endif
 #ifndef FA_DMA_LATE
 #define FA_DMA_LATE 1
@@ -109,11 +110,12 @@
 #endif
 constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
 constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
-    return (FA_ROWSUM16_MASK & d_bit(d)) != 0 && (mode == 0 || d > 32) && !tail && !strided;
+    return (FA_ROWSUM16_MASK & d_bit(d)) != 0 && (d > 32 || (mode == 0 && !tail && !strided));
 }
-// launch bound (waves per SIMD) of an instantiation: the RS16 kernels are sized for four
+// launch bound (waves per SIMD) of an instantiation: the RS16 kernels keep the occupancy the
+// VALU-sum kernels reach (d = 32: four, d = 64: three)
 constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
-    return rs16_on(d, mode, tail, strided) && d <= 32 ? 4 : fa::waves_per_simd(d);
+    return rs16_on(d, mode, tail, strided) && d <= 32 ? 4 : rs16_on(d, mode, tail, strided) && d == 64 ? 3 : fa::waves_per_simd(d);
 }
 #ifndef FA_RSRC32
 #define FA_RSRC32 1

@@ -14,7 +14,7 @@ import torch
 
 CFG = {"c2": (32, 8, 1024, 32), "c3": (32, 8, 1024, 128), "c3s": (32, 8, 4096, 128),
        "c4": (32, 8, 4096, 128), "d256": (32, 8, 1024, 256), "d64": (32, 8, 1024, 64),
-       "l512": (32, 8, 512, 128), "l2048": (32, 8, 2048, 128), "l8192": (8, 8, 8192, 128)}
+       "c3r": (32, 8, 1000, 128), "l512": (32, 8, 512, 128), "l2048": (32, 8, 2048, 128), "l8192": (8, 8, 8192, 128)}
 
 
 def main():
