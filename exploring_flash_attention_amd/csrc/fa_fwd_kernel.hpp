@@ -138,6 +138,12 @@ constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
 #ifndef FA_QSPLIT_MASK
 #define FA_QSPLIT_MASK 0
 #endif
+// FA_PK_SPLIT: in the packed exponent path, a 32-key block's FMAs all ahead of its
+// exponentials (hipcc otherwise puts each v_exp_f32 right behind the v_pk_fma_f32 that feeds
+// it, one hazard s_nop each): C2 +2 %, bitwise-equal outputs
+#ifndef FA_PK_SPLIT
+#define FA_PK_SPLIT 1
+#endif
 #ifndef FA_PK_MAXD
 #define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
 #endif
@@ -420,7 +426,21 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             for (int r = 0; r < RB; ++r) {
                 const f32x2 c2 = {c, c}, nm2 = {-m[r], -m[r]};
 #pragma unroll
-                for (int b2 = 0; b2 < NKB; ++b2)
+                for (int b2 = 0; b2 < NKB; ++b2) {
+                    if constexpr (FA_PK_SPLIT && !QSCALE) {
+                        // all FMAs of the block first: no exponential right behind the FMA
+                        // that feeds it (a hazard wait state each)
+#pragma unroll
+                        for (int i = 0; i < 16; i += 2) {
+                            f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
+                            x = __builtin_elementwise_fma(x, c2, nm2);
+                            s[r][b2][i] = x[0];
+                            s[r][b2][i + 1] = x[1];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) s[r][b2][i] = __builtin_amdgcn_exp2f(s[r][b2][i]);
+                        continue;
+                    }
 #pragma unroll
                     for (int i = 0; i < 16; i += 2) {
                         f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
@@ -428,6 +448,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
                         s[r][b2][i] = __builtin_amdgcn_exp2f(x[0]);
                         s[r][b2][i + 1] = __builtin_amdgcn_exp2f(x[1]);
                     }
+                }
             }
             return;
         }
