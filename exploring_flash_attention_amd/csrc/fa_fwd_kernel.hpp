@@ -117,6 +117,16 @@ constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
 constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
     return rs16_on(d, mode, tail, strided) && d <= 32 ? 4 : rs16_on(d, mode, tail, strided) && d == 64 ? 3 : fa::waves_per_simd(d);
 }
+
+// FA_PP: the d = 128 final no-tail kernel as a ping-pong of two 4-wave groups in one 8-wave
+// workgroup (build with -DFA_WAVES=8; see the PP loop)
+#ifndef FA_PP
+#define FA_PP 0
+#endif
+// FA_PP_PRIO: static s_setprio 1 for ping-pong group A (1) or B (2) through the loop
+#ifndef FA_PP_PRIO
+#define FA_PP_PRIO 0
+#endif
 #ifndef FA_RSRC32
 #define FA_RSRC32 1
 #endif
@@ -206,6 +216,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     constexpr bool QSCALE = (FA_QSCALE_MASK & d_bit(D)) != 0 || QSPLIT;
     constexpr bool FA_MFMA_ROWSUM = D <= FA_MFMA_ROWSUM_MAXD;
     constexpr bool RS16 = rs16_on(D, MODE, TAIL, STRIDED) && !FA_MFMA_ROWSUM;
+    constexpr bool PP = FA_PP && MODE == kFinal && !TAIL && !STRIDED && D == 128 && kWaves == 8 && !QSCALE;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: K ring (2 slots) then V ring (2 slots), one [kBK][D] tile image per slot.
@@ -701,6 +712,92 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 #endif
     };
 
+    // ---- ping-pong halves (PP): the step split at the P.V boundary.  Group A (waves 0-3)
+    // runs H1(0) H2(0) H1(1) ...; group B (waves 4-7, one per SIMD beside an A wave) runs the
+    // same sequence one half-step later, so that on every SIMD one wave's QK^T + exponentials
+    // share the issue port with the other's P.V + row max.  One barrier per half-step; the
+    // DMA of global half-step h (2 pieces per wave) lands by the barrier ending h+1:
+    //   h = 2s: K(s+2) -> K slot s&1      h = 2s+1: V(s+1) -> V slot (s+1)&1
+    // (A: H1(t) issues K(t+2), H2(t) V(t+1); B: H1(t) V(t+1), H2(t) K(t+3)).  Each slot's
+    // previous tile was last read two barriers earlier, so two-slot rings suffice.
+    // (steady loop: this half-step's 2 pieces stay in flight; the tail, whose code hipcc may
+    // spill around -- scratch ops count in vmcnt too -- drains everything)
+    auto pp_bar = [&](auto drain_c) {
+        static_assert(!PP || DPW == 2, "ping-pong waits count two DMA pieces per half-step");
+        // (sched_barriers: hipcc would otherwise sink register-only work such as MFMAs across it)
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (decltype(drain_c)::value)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto half1 = [&](auto par_c, auto more_c, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
+                     const float (&mx)[RB], v8 (&pb)[RB][NKB][2], auto dma) {
+        constexpr int P = decltype(par_c)::value;
+        constexpr bool MORE = decltype(more_c)::value;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            if (__builtin_amdgcn_ballot_w64(mx[r] > m[r] + kThr)) {
+                const float m_new = fmaxf(m[r], mx[r]);
+                const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
+                m[r] = m_new;
+                l[r] *= alpha;
+                if constexpr (RS16)
+                    ls16[r] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
+            }
+        }
+        dma();
+        if constexpr (MORE) qk(kring + (1 - P) * TILEB, sn);
+        exp_tile(sc);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int b2 = 0; b2 < NKB; ++b2)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    u32x4 u;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        u[j] = pack2<T>(sc[r][b2][8 * ss + 2 * j], sc[r][b2][8 * ss + 2 * j + 1]);
+                    pb[r][b2][ss] = __builtin_bit_cast(v8, u);
+                }
+    };
+    auto half2 = [&](auto par_c, auto more_c, f32x16 (&sn)[RB][NKB], float (&mx)[RB],
+                     const v8 (&pb)[RB][NKB][2], auto dma) {
+        constexpr bool MORE = decltype(more_c)::value;
+        dma();
+        u32x2 vcur[2][2], vnext[2][2];
+        read_v(par_c, std::integral_constant<int, 0>{}, vcur, vbase0, vbase1);
+        vwait(vcur);
+        static_for<NKB * NDB>([&](auto i_c) {
+            constexpr int I = decltype(i_c)::value;
+            constexpr int B2 = I / NDB, DB = I % NDB;
+            if constexpr (I + 1 < NKB * NDB)
+                read_v(par_c, std::integral_constant<int, I + 1>{}, vnext, vbase0, vbase1);
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                const u32x4 vv = {vcur[ss][0][0], vcur[ss][0][1], vcur[ss][1][0], vcur[ss][1][1]};
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
+                    if constexpr (RS16 && DB == 0) ls16[r] = M::mma16(sel16, pb[r][B2][ss], ls16[r]);
+                }
+            }
+            if constexpr (I + 1 < NKB * NDB) {
+                vwait(vnext);
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    vcur[ss][0] = vnext[ss][0];
+                    vcur[ss][1] = vnext[ss][1];
+                }
+            }
+        });
+        if constexpr (MORE) rowmax(sn, mx);
+    };
+
     // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
     dma_tile(kbase, kring, 0);
     dma_tile(vbase, vring, 0);
@@ -746,7 +843,69 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
     FA_STAMP(2);
 
-    {
+    if constexpr (PP) {
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using Y = std::integral_constant<bool, true>;
+        using N = std::integral_constant<bool, false>;
+        auto run = [&](auto g_c) {
+            constexpr int G = decltype(g_c)::value;  // 0: group A, 1: group B (half a step behind)
+            v8 pb[RB][NKB][2];
+            auto dk = [&](int t, auto slot_c) { dma_tile(kbase, kring + decltype(slot_c)::value * TILEB, t); };
+            auto dv = [&](int t, auto slot_c) { dma_tile(vbase, vring + decltype(slot_c)::value * TILEB, t); };
+            // H1(t) / H2(t) with t's parity P and this group's DMA share
+            auto h1 = [&](auto par_c, auto more_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB]) {
+                constexpr int P = decltype(par_c)::value;
+                half1(par_c, more_c, sc, sn, mx, pb, [&] {
+                    if constexpr (G == 0) dk(t + 2, std::integral_constant<int, P>{});
+                    else dv(t + 1, std::integral_constant<int, 1 - P>{});
+                });
+            };
+            auto h2 = [&](auto par_c, auto more_c, int t, f32x16 (&sn)[RB][NKB]) {
+                constexpr int P = decltype(par_c)::value;
+                half2(par_c, more_c, sn, mx, pb, [&] {
+                    if constexpr (G == 0) dv(t + 1, std::integral_constant<int, 1 - P>{});
+                    else dk(t + 3, std::integral_constant<int, 1 - P>{});
+                });
+            };
+            if constexpr (FA_PP_PRIO == G + 1) __builtin_amdgcn_s_setprio(1);
+            if constexpr (G == 1) {
+                dk(2, C0{});
+                pp_bar(Y{});
+            }
+            int t = 0;
+            for (; t + 2 < ntiles; t += 2) {
+                h1(C0{}, Y{}, t, sa, sb);
+                pp_bar(N{});
+                h2(C0{}, Y{}, t, sb);
+                pp_bar(N{});
+                h1(C1{}, Y{}, t + 1, sb, sa);
+                pp_bar(N{});
+                h2(C1{}, Y{}, t + 1, sa);
+                pp_bar(N{});
+            }
+            if (ntiles - t == 2) {
+                h1(C0{}, Y{}, t, sa, sb);
+                pp_bar(Y{});
+                h2(C0{}, Y{}, t, sb);
+                pp_bar(Y{});
+                h1(C1{}, N{}, t + 1, sb, sa);
+                pp_bar(Y{});
+                h2(C1{}, N{}, t + 1, sa);
+            } else {
+                h1(C0{}, N{}, t, sa, sb);
+                pp_bar(Y{});
+                h2(C0{}, N{}, t, sb);
+            }
+            // A's last barrier pairs with B's after its last H1; B ends without one.  Every
+            // DMA (including the zero-filled ones past the last tile) lands before the exit.
+            if constexpr (G == 0) pp_bar(Y{});
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (FA_PP_PRIO == G + 1) __builtin_amdgcn_s_setprio(0);
+        };
+        if (__builtin_amdgcn_readfirstlane(tid >> 8)) run(std::integral_constant<int, 1>{});
+        else run(std::integral_constant<int, 0>{});
+    } else {
         using C0 = std::integral_constant<int, 0>;
         using C1 = std::integral_constant<int, 1>;
         // flags: 1 = MORE, 2 = MASKNEXT, 4 = DMAK (see step)
