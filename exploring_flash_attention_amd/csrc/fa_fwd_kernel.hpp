@@ -80,6 +80,10 @@
 #ifndef FA_SGB
 #define FA_SGB 0
 #endif
+// FA_IGLP: __builtin_amdgcn_iglp_opt(FA_IGLP - 1) in the steady step (0 = none)
+#ifndef FA_IGLP
+#define FA_IGLP 0
+#endif
 #ifndef FA_ABL_NODMAWAIT
 #define FA_ABL_NODMAWAIT 0
 #endif
@@ -698,6 +702,9 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
                 __builtin_amdgcn_sched_group_barrier(0x002, VP, 0);
             });
         }
+#endif
+#if FA_IGLP
+        if constexpr (MORE) __builtin_amdgcn_iglp_opt(FA_IGLP - 1);
 #endif
 #if FA_ABL_NOBAR
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
