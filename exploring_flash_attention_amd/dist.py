@@ -107,6 +107,10 @@ def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=None,
     if L % world:
         raise ValueError(f"L={L} must be divisible by world size {world}")
     Lc = L // world
+    if world > 1 and overlap and q.is_cuda and dist.get_backend(group) != "nccl":
+        # gloo's send/recv take host memory only (its all_to_all / all_gather stage device
+        # tensors): device tensors on a non-RCCL group take the all-to-all path
+        overlap = False
     if world > 1 and overlap:
         o_recv, lse_recv = _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc)
         o_local = _combine_fn(o_recv, lse_recv, B, H, q.dtype)

@@ -43,7 +43,7 @@ def _worker(rank, world, port, path, dtype_name):
     dev = torch.device("cuda", 0)
     qg = q.to(dev)
     ks, vs = k[:, :, lo:hi].contiguous().to(dev), v[:, :, lo:hi].contiguous().to(dev)
-    local = fdist.splitkv_attention(qg, ks, vs, overlap=False)
+    local = fdist.splitkv_attention(qg, ks, vs)  # default overlap: a gloo group takes all-to-all
     full = fdist.splitkv_attention(qg, ks, vs, overlap=False, gather=True)
     torch.cuda.synchronize()
     rows = slice(rank * (L // world), (rank + 1) * (L // world))
