@@ -54,6 +54,7 @@ def _worker(rank, world, port, path, dtype_name):
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(300, method="thread")  # a stuck rendezvous fails the test instead of hanging the run
 @pytest.mark.parametrize("dtype_name", ["bfloat16", "float16"])
 @pytest.mark.parametrize("world", [2, 4])
 def test_splitkv_ranks_share_one_gpu(tmp_path, world, dtype_name):
