@@ -2,6 +2,9 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+    (`python bench.py --gpus N` with N > 1 and no launcher starts the N ranks itself, before
+    any GPU work; fewer than N GPUs on the node, or a WORLD_SIZE that disagrees with --gpus,
+    is an error with a non-zero exit status, never a one-GPU line)
     python bench.py --mode splitkv-dist ...   (C5: one sequence's keys sharded over ranks)
 
 Default workload (N=1): config C3 of BASELINE.json -- FA-v1 fused forward, B=32 H=8 L=1024
@@ -209,14 +212,17 @@ def c5_step(torch, fdist, dev, world, rank, impl="torch"):
     else:
         def step():
             fdist.splitkv_attention(q, k, v)
-        kernel = "fa_fwd_kernel (partial) + all_to_all + fa_combine_kernel"
+        kernel = ("fa_fwd_kernel (partial, one launch per destination chunk) + pipelined RCCL send/recv + "
+                  "fa_combine_kernel" if world > 1 else "fa_fwd_kernel (partial) + fa_combine_kernel")
     return step, kernel, flops(B, H, L, d, Lk=hi - lo)
 
 
 def c5_breakdown(torch, ops, fdist, dev, world, rank, barrier):
-    """C5 on this rank without the exchange: the partial kernels over all L query rows
-    (one launch, all-to-all send layout) and the combine of W received partials for the
-    rank's L/W rows, each timed alone; bytes per rank that cross xGMI."""
+    """C5 on this rank, each stage timed alone: the partial kernel over all L query rows (one
+    launch, the all-to-all send layout), the exchange of those partials between the ranks
+    (N > 1: W-1 shifted RCCL send/recv steps posted together, dist.exchange_partials -- the
+    xGMI traffic alone, no kernel beside it), and the combine of the W received partials for the
+    rank's L/W rows.  Bytes per rank that cross xGMI, and the rate the exchange moved them at."""
     cc = CONFIGS["c5"]
     B, H, L, d = cc["B"], cc["H"], cc["L"], cc["d"]
     lo, hi = fdist.shard_bounds(L, world, rank)
@@ -228,14 +234,84 @@ def c5_breakdown(torch, ops, fdist, dev, world, rank, barrier):
     n = 5
     _, p_ms = time_step(torch, lambda: ops.attention_partial(q, k, v, chunk_rows=Lc, partial_dtype=pd,
                                                              o_part=o_part, lse=lse), n, 2, barrier)
-    out = torch.empty(B, H, Lc, d, dtype=q.dtype, device=dev)
-    _, c_ms = time_step(torch, lambda: ops.combine(o_part, lse, B, H, q.dtype, out=out), n, 2, barrier)
+    del q, k, v
+    out = torch.empty(B, H, Lc, d, dtype=torch.bfloat16, device=dev)
+    _, c_ms = time_step(torch, lambda: ops.combine(o_part, lse, B, H, torch.bfloat16, out=out), n, 2, barrier)
     p_ms, c_ms = p_ms / n, c_ms / n
     c_bytes = o_part.numel() * 2 + lse.numel() * 4 + out.numel() * 2
     x_bytes = (world - 1) * (o_part[0].numel() * 2 + lse[0].numel() * 4)
-    return {"partial_ms": round(p_ms, 3), "combine_ms": round(c_ms, 4),
-            "combine_gbps": round(c_bytes / (c_ms * 1e-3) / 1e9, 1),
-            "exchange_bytes_per_rank": int(x_bytes), "partial_format": "fp16 scaled per row"}
+    rec = {"partial_ms": round(p_ms, 3), "combine_ms": round(c_ms, 4),
+           "combine_gbps": round(c_bytes / (c_ms * 1e-3) / 1e9, 1),
+           "exchange_bytes_per_rank": int(x_bytes), "partial_format": "fp16 scaled per row"}
+    if world > 1:
+        o_recv, lse_recv = torch.empty_like(o_part), torch.empty_like(lse)
+
+        def xchg():
+            for w in fdist.exchange_partials(o_part, lse, o_recv, lse_recv):
+                w.wait()
+        _, x_ms = time_step(torch, xchg, n, 2, barrier)
+        x_ms /= n
+        rec.update(exchange_ms=round(x_ms, 3), exchange_gbps=round(x_bytes / (x_ms * 1e-3) / 1e9, 1),
+                   exchange="W-1 shifted send/recv steps posted together (each rank sends and receives "
+                            "exchange_bytes_per_rank; gbps = those bytes / exchange_ms, per rank)")
+    return rec
+
+
+# Split-KV shapes: C4 itself (KV_TILES_PER_BLOCK = 4) under the library's grouping, with the
+# grouping forced (4 and 1 key blocks per workgroup: 4 / 16 partials per query tile) and the
+# automatic split; and two low-parallelism shapes -- the regime the reference's split-KV exists
+# for (flash_attention_v2/README.md:7-21) -- where the library itself splits, each against the
+# same shape forced onto one workgroup per query tile (blocks_per_workgroup = all blocks).
+EXTRA_SHAPES = (
+    # name, B, H, L, d, variant, kv_tiles_per_block, blocks_per_workgroup
+    ("c2_fused", 32, 8, 1024, 32, "v1", None, None),
+    ("c4_splitkv", 32, 8, 4096, 128, "v2", 4, None),
+    ("c4_splitkv_4_blocks_per_wg", 32, 8, 4096, 128, "v2", 4, 4),
+    ("c4_splitkv_1_block_per_wg", 32, 8, 4096, 128, "v2", 4, 1),
+    ("c4_splitkv_auto", 32, 8, 4096, 128, "v2", "auto", None),
+    ("b2h2_l16k_splitkv", 2, 2, 16384, 128, "v2", 4, None),
+    ("b2h2_l16k_unsplit", 2, 2, 16384, 128, "v2", 4, "all"),
+    ("b1h2_l16k_splitkv", 1, 2, 16384, 128, "v2", 4, None),
+    ("b1h2_l16k_unsplit", 1, 2, 16384, 128, "v2", 4, "all"),
+)
+
+
+def single_gpu_extras(torch, ops, dev, barrier, names=None):
+    """bench extras at N = 1: ms, TFLOP/s and the split plan of each EXTRA_SHAPES entry."""
+    out = {}
+    for name, B, H, L, d, fn, kvt, grp in EXTRA_SHAPES:
+        if names is not None and name not in names:
+            continue
+        qq, kk, vv = _make_inputs(torch, dev, B, H, L, d, seed=7)
+        rec = {"B": B, "H": H, "L": L, "d": d}
+        if fn == "v1":
+            def st():
+                ops.attention_v1(qq, kk, vv)
+        else:
+            if grp == "all":  # every key block of a query tile on one workgroup: no split
+                grp = ops.v2_split_plan(B, H, L, d, kvt, qq.dtype)[0]
+            nb, _ = ops.v2_workspace_bytes(B, H, L, d, kvt, qq.dtype, blocks_per_workgroup=grp)
+            plan = ops.v2_split_plan(B, H, L, d, kvt, qq.dtype, blocks_per_workgroup=grp)
+            wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
+            oo = torch.empty_like(qq)
+
+            def st():
+                ops.attention_v2(qq, kk, vv, kvt, out=oo, workspace=wsx, blocks_per_workgroup=grp)
+            rec.update(kv_tiles_per_block=kvt, key_blocks=plan[0], blocks_per_workgroup=plan[1],
+                       partials_per_tile=plan[2], workspace_bytes=nb)
+        f = flops(B, H, L, d)
+        n = max(10, min(50, int(2e13 / f)))  # >= ~20 TFLOP of work per timing window
+        _, ems = time_step(torch, st, n, max(3, n // 3), barrier)
+        ms = ems / n
+        rec.update(ms=round(ms, 4), tflops=round(f / (ms * 1e-3) / 1e12, 1),
+                   frac=round(f / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4))
+        out[name] = rec
+        del qq, kk, vv
+    for base in ("b2h2_l16k", "b1h2_l16k"):  # split against unsplit, same shape
+        if f"{base}_splitkv" in out and f"{base}_unsplit" in out:
+            out[f"{base}_splitkv"]["speedup_vs_unsplit"] = round(
+                out[f"{base}_unsplit"]["ms"] / out[f"{base}_splitkv"]["ms"], 3)
+    return out
 
 
 def load_traffic(config):
@@ -277,6 +353,38 @@ def output_check(torch, q, k, v, out, n=16):
 WATCHDOG_EXIT = 3
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n, script, script_args, env=None):
+    """Run `script` as n ranks of one node (torch.distributed.run, rendezvous on 127.0.0.1)
+    as a CHILD process -- never an exec -- and return its exit status: non-zero when any rank
+    fails (torch.distributed.run reports a failed rank and exits non-zero)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script, *script_args]
+    return subprocess.call(cmd, env=dict(os.environ if env is None else env))
+
+
+def self_launch(gpus, argv):
+    """`bench.py --gpus N` (N > 1) without a launcher: start N ranks before any GPU work.  A
+    box with fewer than N GPUs is an error, never a silent one-GPU line.  (Counting devices
+    does not initialise the GPU on this image.)"""
+    import torch
+    have = torch.cuda.device_count()
+    if have < gpus:
+        print(f"bench: --gpus {gpus} requested but this node has {have} GPU(s); refusing to report a "
+              f"{have}-GPU number as a {gpus}-GPU one", file=sys.stderr, flush=True)
+        return 2
+    print(f"bench: launching {gpus} ranks (torch.distributed.run, one process per GPU)", file=sys.stderr,
+          flush=True)
+    return spawn_ranks(gpus, os.path.abspath(__file__), argv)
+
+
 def start_watchdog(seconds, rank, partial_line):
     """After `seconds`: print partial_line() (rank 0's JSON line with the error recorded, or
     None) and leave the process with status WATCHDOG_EXIT -- a hung exchange is a failed run
@@ -313,11 +421,17 @@ def main():
                     help="seconds of untimed forwards before any timing (clock settle; 0 = off)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the request disagree",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
 
     cfg = CONFIGS["c5"] if args.mode == "splitkv-dist" else CONFIGS[args.config]
     B, H, L, d = cfg["B"], cfg["H"], cfg["L"], cfg["d"]
@@ -367,38 +481,7 @@ def main():
         # before the headline, so the headline's window also finds the clock settled.
         # (C3's tiled-d form is the same launch as the headline: fa_fwd_v1_tiled_d validates
         # the d tiles and runs the fused kernel)
-        # C4 (KV_TILES_PER_BLOCK = 4: 16 key blocks of 256 keys per query tile) as scheduled
-        # by the library (blocks of a query tile grouped on workgroups, fa_fwd_v2_split_plan),
-        # with the group fixed at 4 and at 1 (FA_SPLIT_GROUP: every block its own workgroup
-        # and HBM partial), and the occupancy-chosen split
-        for name, c, fn, grp in (("c2_fused", "c2", "v1", None), ("c4_splitkv", "c4", "v2", None),
-                                 ("c4_splitkv_4_blocks_per_wg", "c4", "v2", "4"),
-                                 ("c4_splitkv_1_block_per_wg", "c4", "v2", "1"),
-                                 ("c4_splitkv_auto", "c4", "v2auto", None)):
-            cc = CONFIGS[c]
-            qq, kk, vv = _make_inputs(torch, dev, cc["B"], cc["H"], cc["L"], cc["d"], seed=7)
-            if grp is not None:
-                os.environ["FA_SPLIT_GROUP"] = grp
-            if fn == "v1":
-                def st():
-                    ops.attention_v1(qq, kk, vv)
-            else:  # KV_TILES_PER_BLOCK = 4 as in C4, or the occupancy-chosen split
-                kvt = 4 if fn == "v2" else "auto"
-                nb, nsp = ops.v2_workspace_bytes(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
-                plan = ops.v2_split_plan(cc["B"], cc["H"], cc["L"], cc["d"], kvt, qq.dtype)
-                wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
-
-                def st():
-                    ops.attention_v2(qq, kk, vv, kvt, workspace=wsx)
-            n = 50
-            _, ems = time_step(torch, st, n, 20, barrier)
-            os.environ.pop("FA_SPLIT_GROUP", None)
-            f = flops(cc["B"], cc["H"], cc["L"], cc["d"])
-            extra[name] = {"ms": round(ems / n, 4), "tflops": round(f / (ems / n * 1e-3) / 1e12, 1)}
-            if fn.startswith("v2"):
-                extra[name].update(key_blocks=plan[0], blocks_per_workgroup=plan[1], partials_per_tile=plan[2],
-                                   workspace_bytes=nb)
-            del qq, kk, vv
+        extra.update(single_gpu_extras(torch, ops, dev, barrier))
         torch.cuda.empty_cache()
 
     check = None
@@ -415,7 +498,10 @@ def main():
 
             def step():
                 ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
-            kernel = "fa_fwd_kernel (split-KV, in-kernel combine)"
+            _, _, ppt = ops.v2_split_plan(B, H, L, d, cfg["kvtpb"], q.dtype)
+            kernel = ("fa_fwd_kernel (split-KV, in-kernel combine)" if ppt > 1
+                      else "fa_fwd_kernel (final: the library groups every key block of a query tile "
+                           "on one workgroup, fa_fwd_v2_split_plan)")
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         work = flops(B, H, L, d)
         workload = ("FA-v1 fused / tiled-d forward (one kernel)" if cfg["variant"] == "v1"
@@ -502,10 +588,14 @@ def main():
             del st5
             torch.cuda.empty_cache()
             bd = c5_breakdown(torch, ops, fdist, dev, world, rank, barrier)
-            tb = torch.tensor([bd["partial_ms"], bd["combine_ms"]], device=dev, dtype=torch.float64)
+            keys = [k_ for k_ in ("partial_ms", "combine_ms", "exchange_ms") if k_ in bd]
+            tb = torch.tensor([bd[k_] for k_ in keys], device=dev, dtype=torch.float64)
             if world > 1:
                 dist.all_reduce(tb, op=dist.ReduceOp.MAX)
-            bd["partial_ms"], bd["combine_ms"] = round(float(tb[0]), 3), round(float(tb[1]), 4)
+            for i, k_ in enumerate(keys):
+                bd[k_] = round(float(tb[i]), 4)
+            if "exchange_ms" in bd:
+                bd["exchange_gbps"] = round(bd["exchange_bytes_per_rank"] / (bd["exchange_ms"] * 1e-3) / 1e9, 1)
             extra["c5_splitkv_dist"]["breakdown_max_over_ranks"] = bd
         except Exception as exc:  # noqa: BLE001 -- reported, the headline stands
             extra["c5_splitkv_dist"] = {"error": f"{type(exc).__name__}: {exc}"[:300], "ranks": world}

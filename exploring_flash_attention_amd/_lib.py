@@ -24,6 +24,7 @@ FA_DTYPE_FP64 = 3
 FA_DTYPE_FP16_SCALED = 4  # split-KV partials: fp16 scaled per row by a power of two
 
 FA_KV_TILES_AUTO = -1  # kv_tiles_per_block: split chosen from the device's occupancy
+FA_BLOCKS_PER_WG_AUTO = 0  # blocks_per_workgroup: the library groups the key blocks itself
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -39,16 +40,17 @@ SIGNATURES = {
     "fa_fwd_v1": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
     "fa_fwd_v1_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, ctypes.c_double, _I, _P]),
     "fa_fwd_v1_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, ctypes.c_double, _I, _P]),
-    "fa_fwd_v1_w64": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
     "fa_fwd_v1_tiled_d": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P]),
-    "fa_fwd_v2_split_plan": (_I, [_I64, _I64, _I64, _I64, _I, _I, _PI, _PI, _PI]),
+    "fa_fwd_v2_split_plan": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I, _PI, _PI, _PI]),
     "fa_fwd_v2_workspace_size": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I,
                                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_I)]),
+    "fa_fwd_v2_workspace_size_ex": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I, _I,
+                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_I)]),
     "fa_fwd_v2": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
                        _I, _I, _P]),
     "fa_fwd_v2_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
                               ctypes.c_double, _I, _I, _P]),
-    "fa_fwd_v2_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P, ctypes.c_size_t,
+    "fa_fwd_v2_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _P, ctypes.c_size_t,
                           _P, _P, _P, ctypes.c_double, _I, _I, _P]),
     "fa_fwd_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
     "fa_fwd_partial_ex": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I, _I, _P]),

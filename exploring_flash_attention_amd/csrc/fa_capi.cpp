@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <atomic>
 
 #include "../../include/fa_mi355x.h"
 #include "fa_internal.hpp"
@@ -189,15 +190,29 @@ V2Layout v2_layout(int64_t BH, int64_t L, int64_t d, int ns, fa::Elem pe) {
     return w;
 }
 
-// Workgroups the device runs at once (forward kernel occupancy: 2 per CU, 1 at d = 256).
-int resident_workgroups(int64_t d) {
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) {
+// Compute units of the current device, queried once per device (the split planner runs on
+// every fa_fwd_v2 call).  No device (CPU-only tests): the MI355X's 256.
+int device_cus() {
+    static std::atomic<int> cached[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
         (void)hipGetLastError();
-        ncu = 256;  // MI355X
+        return 256;
     }
-    return ncu * fa::waves_per_simd((int)d);
+    int n = cached[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 256;
+    }
+    cached[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
+
+// Workgroups of the split kernel (fused split mode, contiguous, with a key tail) the device
+// runs at once: the kernel's own launch bound (fa_internal.hpp kernel_wps) per CU.
+int resident_workgroups(int64_t d) {
+    return device_cus() * fa::kernel_wps((int)d, fa::kFused, true, false);
 }
 
 // FA_KV_TILES_AUTO: pick the split from occupancy -- no split when the
@@ -220,26 +235,34 @@ int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
 // (flash_attention_v2/CUDA/flash_attention_v2.h:243, :356).  Here consecutive blocks of a
 // query tile are grouped onto one workgroup: the blocks of a group are combined on chip (the
 // online softmax carried across them -- algebraically the reduction's formula, split after
-// split), the groups' partials through the workspace and the in-kernel reduction.  As many
-// blocks go to one group as still leave >= 4 workgroups per resident slot, so a problem whose
-// query tiles already fill the GPU moves no partials through HBM at all, and a short-batch
-// long-sequence one gets one workgroup per block.  FA_SPLIT_GROUP=<n> (environment) fixes
-// the group size for measurements (1 = one workgroup and one HBM partial per block).
+// split), the groups' partials through the workspace and the in-kernel reduction.  By default
+// (blocks_per_workgroup = FA_BLOCKS_PER_WG_AUTO) as many blocks go to one group as still leave
+// >= 4 workgroups per resident slot, so a problem whose query tiles already fill the GPU moves
+// no partials through HBM at all, and a short-batch long-sequence one gets one workgroup per
+// block; a positive blocks_per_workgroup fixes the group (1 = the reference's layout: one
+// workgroup and one HBM partial per block).  Planned once per call: the workspace size, the
+// grid and the split length all come from the same SplitPlan.
 struct SplitPlan {
+    int kvtpb;       // KV tiles per key block (FA_KV_TILES_AUTO resolved)
     int units;       // the reference's key blocks: ceil(L / (kv_tiles_per_block * bk))
     int group;       // blocks per workgroup
     int launched;    // partial workgroups per query tile: ceil(units / group)
     int kv_per_wg;   // keys per workgroup (group * block keys, at most L)
 };
-SplitPlan plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, fa::Elem e) {
+int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, fa::Elem e, SplitPlan* out) {
+    if (kvtpb == FA_KV_TILES_AUTO) kvtpb = auto_kv_tiles(BH, L, d, e);
+    if (kvtpb <= 0) return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kvtpb);
+    if (blocks_per_wg < 0)
+        return fail(FA_ERR_INVALID_ARG, "blocks_per_workgroup must be >= 0 (0 = library schedule), got %d",
+                    blocks_per_wg);
     SplitPlan p{};
+    p.kvtpb = kvtpb;
     const int64_t keys = (int64_t)kvtpb * keys_per_tile(e, d);
     p.units = (int)((L + keys - 1) / keys);
     const int64_t items = BH * ((L + rows_per_block(e) - 1) / rows_per_block(e));
     p.group = 1;
-    if (const char* env = std::getenv("FA_SPLIT_GROUP")) {
-        const int g = std::atoi(env);
-        if (g >= 1) p.group = g < p.units ? g : p.units;
+    if (blocks_per_wg > 0) {
+        p.group = blocks_per_wg < p.units ? blocks_per_wg : p.units;
     } else {
         const int64_t want = 4 * (int64_t)resident_workgroups(d);
         for (int g = p.units; g > 1; --g)
@@ -251,7 +274,23 @@ SplitPlan plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, fa::Elem e) {
     p.launched = (p.units + p.group - 1) / p.group;
     const int64_t kw = keys * p.group;
     p.kv_per_wg = (int)(kw < L ? kw : L);
-    return p;
+    *out = p;
+    return FA_OK;
+}
+
+// workspace bytes for a plan (the grid bound checked too)
+int v2_workspace(int64_t B, int64_t H, int64_t L, int64_t d, const SplitPlan& sp, fa::Elem e, fa::Elem pe,
+                 size_t* bytes) {
+    const int ns = sp.launched;
+    // one workgroup per (query tile, split group, b*h): the grid and the kernel's block index
+    // are 32-bit (dim3, xcd_remap), so a grid past 2^31-1 is refused instead of truncated
+    const int64_t nqt = (L + rows_per_block(e) - 1) / rows_per_block(e);
+    if (B * H * nqt > (int64_t)0x7fffffff / ns)
+        return fail(FA_ERR_UNSUPPORTED, "split-KV grid of %lld x %d workgroups exceeds 2^31-1 "
+                    "(raise kv_tiles_per_block)", (long long)(B * H * nqt), ns);
+    // one partial workgroup per query tile: the FA-v1 kernel, no workspace needed
+    *bytes = ns == 1 ? 256 : v2_layout(B * H, L, d, ns, pe).total;
+    return FA_OK;
 }
 
 }  // namespace
@@ -305,19 +344,6 @@ int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     return ok();
 }
 
-int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
-                  int64_t L, int64_t d, int dtype, void* stream) {
-    fa::Elem e;
-    if (int st = check_shape(B, H, L, d)) return st;
-    if (int st = check_dtype(dtype, &e)) return st;
-    if (int st = check_ptrs(q, k, v, o)) return st;
-    if (d != 128 || e == fa::Elem::F64)
-        return fail(FA_ERR_UNSUPPORTED, "the 64-row-wave kernel serves d=128 bf16/fp16 only");
-    fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
-    if (hipError_t he = fa::launch_fwd_w64(e, a, (hipStream_t)stream)) return hip_fail(he, "fa_fwd_v1_w64 launch");
-    return ok();
-}
-
 int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
                       int64_t L, int64_t d, int d_tile_qk, int d_tile_v, int dtype, void* stream) {
     fa::Elem e;
@@ -333,39 +359,35 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o, int6
 
 int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block,
                              int dtype, int partial_dtype, size_t* bytes, int* num_splits) {
+    return fa_fwd_v2_workspace_size_ex(B, H, L, d, kv_tiles_per_block, FA_BLOCKS_PER_WG_AUTO, dtype,
+                                       partial_dtype, bytes, num_splits);
+}
+
+int fa_fwd_v2_workspace_size_ex(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block,
+                                int blocks_per_workgroup, int dtype, int partial_dtype, size_t* bytes,
+                                int* num_splits) {
     fa::Elem e, pe;
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
-    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
-    if (kv_tiles_per_block <= 0)
-        return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
-    const SplitPlan sp = plan_splits(B * H, L, d, kv_tiles_per_block, e);
-    const int ns = sp.launched;
-    // one workgroup per (query tile, split group, b*h): the grid and the kernel's block index
-    // are 32-bit (dim3, xcd_remap), so a grid past 2^31-1 is refused instead of truncated
-    const int64_t nqt = (L + rows_per_block(e) - 1) / rows_per_block(e);
-    if (B * H * nqt > (int64_t)0x7fffffff / ns)
-        return fail(FA_ERR_UNSUPPORTED, "split-KV grid of %lld x %d workgroups exceeds 2^31-1 "
-                    "(raise kv_tiles_per_block)", (long long)(B * H * nqt), ns);
-    // one partial workgroup per query tile: the FA-v1 kernel, no workspace needed
-    *bytes = ns == 1 ? 256 : v2_layout(B * H, L, d, ns, pe).total;
+    SplitPlan sp;
+    if (int st = plan_splits(B * H, L, d, kv_tiles_per_block, blocks_per_workgroup, e, &sp)) return st;
+    if (int st = v2_workspace(B, H, L, d, sp, e, pe, bytes)) return st;
     if (num_splits) *num_splits = sp.units;
     return ok();
 }
 
-int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block, int dtype,
-                         int* key_blocks, int* blocks_per_workgroup, int* partials_per_tile) {
+int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block,
+                         int blocks_per_workgroup, int dtype, int* key_blocks, int* blocks_per_wg_out,
+                         int* partials_per_tile) {
     fa::Elem e;
     if (int st = check_shape(B, H, L, d)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
-    if (kv_tiles_per_block == FA_KV_TILES_AUTO) kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
-    if (kv_tiles_per_block <= 0)
-        return fail(FA_ERR_INVALID_ARG, "kv_tiles_per_block must be positive (got %d)", kv_tiles_per_block);
-    const SplitPlan p = plan_splits(B * H, L, d, kv_tiles_per_block, e);
+    SplitPlan p;
+    if (int st = plan_splits(B * H, L, d, kv_tiles_per_block, blocks_per_workgroup, e, &p)) return st;
     if (key_blocks) *key_blocks = p.units;
-    if (blocks_per_workgroup) *blocks_per_workgroup = p.group;
+    if (blocks_per_wg_out) *blocks_per_wg_out = p.group;
     if (partials_per_tile) *partials_per_tile = p.launched;
     return ok();
 }
@@ -382,33 +404,33 @@ int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o, int64
                      int64_t L, int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
                      void* workspace, size_t workspace_bytes, double softmax_scale, int dtype,
                      int partial_dtype, void* stream) {
-    return fa_fwd_v2_ex(q, k, v, o, B, H, L, d, d_tile_qk, d_tile_v, kv_tiles_per_block, workspace,
-                        workspace_bytes, nullptr, nullptr, nullptr, softmax_scale, dtype, partial_dtype, stream);
+    return fa_fwd_v2_ex(q, k, v, o, B, H, L, d, d_tile_qk, d_tile_v, kv_tiles_per_block, FA_BLOCKS_PER_WG_AUTO,
+                        workspace, workspace_bytes, nullptr, nullptr, nullptr, softmax_scale, dtype, partial_dtype,
+                        stream);
 }
 
 int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H, int64_t L,
-                 int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block, void* workspace,
-                 size_t workspace_bytes, const int64_t* q_strides, const int64_t* kv_strides,
+                 int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block, int blocks_per_workgroup,
+                 void* workspace, size_t workspace_bytes, const int64_t* q_strides, const int64_t* kv_strides,
                  const int64_t* o_strides, double softmax_scale, int dtype, int partial_dtype, void* stream) {
     fa::Elem e, pe;
-    size_t need = 0;
-    int ns = 0;
-    if (kv_tiles_per_block == FA_KV_TILES_AUTO && check_dtype(dtype, &e) == FA_OK)
-        kv_tiles_per_block = auto_kv_tiles(B * H, L, d, e);
-    if (int st = fa_fwd_v2_workspace_size(B, H, L, d, kv_tiles_per_block, dtype, partial_dtype,
-                                          &need, nullptr))
-        return st;
+    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_dtype(dtype, &e)) return st;
+    if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     if (int st = check_d_tiles(d, d_tile_qk, d_tile_v)) return st;
-    check_dtype(dtype, &e);
-    check_partial_dtype(partial_dtype, dtype, &pe);
+    const int64_t BH = B * H;
+    // one plan for the workspace check, the grid and the split length
+    SplitPlan sp;
+    if (int st = plan_splits(BH, L, d, kv_tiles_per_block, blocks_per_workgroup, e, &sp)) return st;
+    size_t need = 0;
+    if (int st = v2_workspace(B, H, L, d, sp, e, pe, &need)) return st;
     if (!workspace || workspace_bytes < need)
         return fail(FA_ERR_WORKSPACE, "workspace of %zu bytes needed, got %zu%s", need, workspace_bytes,
                     workspace ? "" : " (NULL)");
     if ((uintptr_t)workspace & 255) return fail(FA_ERR_WORKSPACE, "workspace must be 256-byte aligned");
 
-    const int64_t BH = B * H;
-    ns = plan_splits(BH, L, d, kv_tiles_per_block, e).launched;
+    const int ns = sp.launched;
     fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
     if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
@@ -419,7 +441,7 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     }
     const V2Layout w = v2_layout(BH, L, d, ns, pe);
     a.nsplit = ns;
-    a.kv_per_split = plan_splits(BH, L, d, kv_tiles_per_block, e).kv_per_wg;
+    a.kv_per_split = sp.kv_per_wg;
     if (e == fa::Elem::F64) {  // fp64: the reference's two kernels (partial, then reduction)
         a.o = workspace;
         a.lse64 = (double*)((char*)workspace + w.lse_off);

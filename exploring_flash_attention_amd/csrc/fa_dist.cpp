@@ -1,6 +1,7 @@
 // fa_dist.cpp -- multi-GPU split-KV forward over RCCL (include/fa_mi355x_dist.h).
-// Host orchestration only: the kernels are libfa_mi355x.so's fa_fwd_partial / fa_combine,
-// the exchange is one grouped RCCL send/recv round over xGMI.
+// Host orchestration only: the kernels are libfa_mi355x.so's fa_fwd_partial_ex / fa_combine,
+// the exchange is RCCL send/recv over xGMI on the communicator's own stream, so that the
+// transfer of one destination's partials overlaps the next destination's partial kernel.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -8,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/fa_mi355x_dist.h"
 
@@ -34,7 +36,26 @@ int ok() {
 int rccl_fail(ncclResult_t r, const char* what) {
     return fail(FA_ERR_RCCL, "%s: %s", what, ncclGetErrorString(r));
 }
+int hip_fail(hipError_t e, const char* what) { return fail(FA_ERR_HIP, "%s: %s", what, hipGetErrorString(e)); }
 int core_fail(int st, const char* what) { return fail(st, "%s: %s", what, fa_last_error()); }
+
+// The communicator handle: the RCCL communicator plus what the pipelined exchange needs,
+// all created once at fa_dist_comm_init (the forward itself never allocates): a stream for
+// the RCCL operations and one event per destination step (+ one for "exchange done").
+struct Comm {
+    ncclComm_t nccl = nullptr;
+    int world = 0, rank = 0, device = 0;
+    hipStream_t xstream = nullptr;
+    std::vector<hipEvent_t> ev;  // ev[s], s = 1..world-1: partial of step s queued; ev[0]: exchange done
+    bool broken = false;         // an RCCL enqueue failed after others were posted
+};
+
+void destroy(Comm* c) {
+    for (hipEvent_t e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->xstream) (void)hipStreamDestroy(c->xstream);
+    delete c;
+}
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -83,15 +104,37 @@ int fa_dist_comm_init(void** comm, int world, int rank, const void* id) {
         return fail(FA_ERR_INVALID_ARG, "bad rank %d / world %d", rank, world);
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    ncclComm_t c = nullptr;
-    if (ncclResult_t r = ncclCommInitRank(&c, world, u, rank)) return rccl_fail(r, "ncclCommInitRank");
+    Comm* c = new Comm;
+    c->world = world;
+    c->rank = rank;
+    if (hipError_t he = hipGetDevice(&c->device)) {
+        destroy(c);
+        return hip_fail(he, "hipGetDevice");
+    }
+    if (hipError_t he = hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking)) {
+        destroy(c);
+        return hip_fail(he, "exchange stream");
+    }
+    c->ev.assign(world, nullptr);
+    for (int i = 0; i < world; ++i)
+        if (hipError_t he = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming)) {
+            destroy(c);
+            return hip_fail(he, "exchange events");
+        }
+    if (ncclResult_t r = ncclCommInitRank(&c->nccl, world, u, rank)) {
+        destroy(c);
+        return rccl_fail(r, "ncclCommInitRank");
+    }
     *comm = c;
     return ok();
 }
 
 int fa_dist_comm_destroy(void* comm) {
     if (!comm) return ok();
-    if (ncclResult_t r = ncclCommDestroy((ncclComm_t)comm)) return rccl_fail(r, "ncclCommDestroy");
+    Comm* c = (Comm*)comm;
+    ncclResult_t r = c->nccl ? ncclCommDestroy(c->nccl) : ncclSuccess;
+    destroy(c);
+    if (r) return rccl_fail(r, "ncclCommDestroy");
     return ok();
 }
 
@@ -113,63 +156,117 @@ int fa_fwd_v2_dist_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, in
 int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void* o, int64_t B,
                    int64_t H, int64_t L, int64_t d, void* comm, int gather, void* workspace,
                    size_t workspace_bytes, int dtype, int partial_dtype, void* stream) {
+    // ---- every check before anything is enqueued (a failure past the first RCCL post would
+    // leave the peers in a half-posted exchange)
     if (!comm) return fail(FA_ERR_INVALID_ARG, "comm is NULL");
-    int world = 0, rank = 0;
-    if (ncclResult_t r = ncclCommCount((ncclComm_t)comm, &world)) return rccl_fail(r, "ncclCommCount");
-    if (ncclResult_t r = ncclCommUserRank((ncclComm_t)comm, &rank)) return rccl_fail(r, "ncclCommUserRank");
+    Comm* c = (Comm*)comm;
+    if (c->broken)
+        return fail(FA_ERR_RCCL, "communicator unusable: an earlier exchange failed part-way (destroy it)");
+    const int world = c->world, rank = c->rank;
     size_t need = 0;
     if (int st = fa_fwd_v2_dist_workspace_size(B, H, L, d, world, dtype, partial_dtype, &need)) return st;
+    if (!q || !k_shard || !v_shard || !o) return fail(FA_ERR_INVALID_ARG, "null tensor pointer");
     if (!workspace || workspace_bytes < need)
         return fail(FA_ERR_WORKSPACE, "workspace of %zu bytes needed, got %zu", need, workspace_bytes);
     if ((uintptr_t)workspace & 255) return fail(FA_ERR_WORKSPACE, "workspace must be 256-byte aligned");
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != c->device)
+        return fail(FA_ERR_INVALID_ARG, "current device %d is not the communicator's device %d", dev, c->device);
     const int64_t BH = B * H, Lc = L / world;
     const Layout w = layout(BH, L, d, dtype, partial_dtype);
     char* ws = (char*)workspace;
     hipStream_t s = (hipStream_t)stream;
-
-    // 1. partials of all L query rows over this rank's keys, in the send layout
-    if (int st = fa_fwd_partial(q, k_shard, v_shard, ws + w.send_o, ws + w.send_lse, B, H, L, Lc, d, Lc,
-                                dtype, partial_dtype, stream))
-        return core_fail(st, "fa_fwd_partial");
-    // 2. chunk p -> rank p (one grouped send/recv round)
     const size_t chunk_o = (size_t)BH * Lc * d * esize(partial_dtype);
     const size_t chunk_l = (size_t)BH * Lc * lsize(dtype, partial_dtype);
-    if (world > 1) {
-        if (ncclResult_t r = ncclGroupStart()) return rccl_fail(r, "ncclGroupStart");
-        const ncclComm_t c = (ncclComm_t)comm;
-        for (int p = 0; p < world; ++p) {
-            ncclResult_t r = ncclSend(ws + w.send_o + p * chunk_o, chunk_o, ncclUint8, p, c, s);
-            if (r == ncclSuccess) r = ncclRecv(ws + w.recv_o + p * chunk_o, chunk_o, ncclUint8, p, c, s);
-            if (r == ncclSuccess) r = ncclSend(ws + w.send_lse + p * chunk_l, chunk_l, ncclUint8, p, c, s);
-            if (r == ncclSuccess) r = ncclRecv(ws + w.recv_lse + p * chunk_l, chunk_l, ncclUint8, p, c, s);
-            if (r != ncclSuccess) {
-                // close the group before reporting: an open group would swallow the next call
-                (void)ncclGroupEnd();
-                char what[64];
-                snprintf(what, sizeof what, "send/recv with rank %d", p);
-                return rccl_fail(r, what);
-            }
+    // pipelined (one partial launch per destination chunk, a q row-range view in place) for
+    // bf16 / fp16; fp64 (no strided kernels) computes all chunks in one launch first
+    const bool pipelined = dtype != FA_DTYPE_FP64 && world > 1 && d % 8 == 0;
+    const int64_t qst[3] = {H * L * d, L * d, d};
+    const size_t qrow_bytes = (size_t)d * esize(dtype);
+    auto partial_chunk = [&](int p, char* o_dst, char* l_dst) {
+        return fa_fwd_partial_ex((const char*)q + (size_t)p * Lc * qrow_bytes, k_shard, v_shard, o_dst, l_dst, B, H,
+                                 Lc, Lc, d, Lc, qst, dtype, partial_dtype, stream);
+    };
+    // one step of the shifted exchange on the exchange stream: send chunk rank+st to rank+st,
+    // receive chunk rank from rank-st (all ranks' links busy at once, every step a matching)
+    auto post_step = [&](int st) -> int {
+        const int dst = (rank + st) % world, src = (rank - st + world) % world;
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess) {
+            // (inside a group RCCL only queues; an error here discards the whole group at
+            // ncclGroupEnd, nothing of it is posted)
+            ncclResult_t e = ncclSend(ws + w.send_o + dst * chunk_o, chunk_o, ncclUint8, dst, c->nccl, c->xstream);
+            if (e == ncclSuccess) e = ncclRecv(ws + w.recv_o + src * chunk_o, chunk_o, ncclUint8, src, c->nccl, c->xstream);
+            if (e == ncclSuccess) e = ncclSend(ws + w.send_lse + dst * chunk_l, chunk_l, ncclUint8, dst, c->nccl, c->xstream);
+            if (e == ncclSuccess) e = ncclRecv(ws + w.recv_lse + src * chunk_l, chunk_l, ncclUint8, src, c->nccl, c->xstream);
+            r = ncclGroupEnd();
+            if (e != ncclSuccess) r = e;
         }
-        if (ncclResult_t r = ncclGroupEnd()) return rccl_fail(r, "send/recv exchange");
+        if (r != ncclSuccess) {
+            if (st > 1) c->broken = true;  // earlier steps are posted: the peers are mid-exchange
+            char what[96];
+            snprintf(what, sizeof what, "exchange step %d (to rank %d, from rank %d)", st, dst, src);
+            return rccl_fail(r, what);
+        }
+        return FA_OK;
+    };
+
+    if (world == 1) {  // nothing to exchange: partial straight into the receive side
+        if (int st = fa_fwd_partial(q, k_shard, v_shard, ws + w.recv_o, ws + w.recv_lse, B, H, L, Lc, d, Lc, dtype,
+                                    partial_dtype, stream))
+            return core_fail(st, "fa_fwd_partial");
+    } else if (pipelined) {
+        for (int st = 1; st < world; ++st) {
+            const int dst = (rank + st) % world;
+            if (int e = partial_chunk(dst, ws + w.send_o + dst * chunk_o, ws + w.send_lse + dst * chunk_l)) {
+                if (st > 1) c->broken = true;
+                return core_fail(e, "fa_fwd_partial_ex");
+            }
+            if (hipError_t he = hipEventRecord(c->ev[st], s)) return hip_fail(he, "hipEventRecord");
+            if (hipError_t he = hipStreamWaitEvent(c->xstream, c->ev[st], 0)) return hip_fail(he, "hipStreamWaitEvent");
+            if (int e = post_step(st)) return e;
+        }
+        // own chunk last, straight into the receive buffer (it never crosses a link)
+        if (int e = partial_chunk(rank, ws + w.recv_o + rank * chunk_o, ws + w.recv_lse + rank * chunk_l)) {
+            c->broken = true;
+            return core_fail(e, "fa_fwd_partial_ex");
+        }
+    } else {
+        // all chunks in one launch (send layout), then the W-1 steps; the own chunk is a local copy
+        if (int st = fa_fwd_partial(q, k_shard, v_shard, ws + w.send_o, ws + w.send_lse, B, H, L, Lc, d, Lc, dtype,
+                                    partial_dtype, stream))
+            return core_fail(st, "fa_fwd_partial");
+        if (hipError_t he = hipEventRecord(c->ev[1], s)) return hip_fail(he, "hipEventRecord");
+        if (hipError_t he = hipStreamWaitEvent(c->xstream, c->ev[1], 0)) return hip_fail(he, "hipStreamWaitEvent");
+        for (int st = 1; st < world; ++st)
+            if (int e = post_step(st)) return e;
+        if (hipError_t he = hipMemcpyAsync(ws + w.recv_o + rank * chunk_o, ws + w.send_o + rank * chunk_o, chunk_o,
+                                           hipMemcpyDeviceToDevice, s))
+            return hip_fail(he, "own chunk copy");
+        if (hipError_t he = hipMemcpyAsync(ws + w.recv_lse + rank * chunk_l, ws + w.send_lse + rank * chunk_l,
+                                           chunk_l, hipMemcpyDeviceToDevice, s))
+            return hip_fail(he, "own chunk copy");
     }
-    const char* ro = world > 1 ? ws + w.recv_o : ws + w.send_o;
-    const char* rl = world > 1 ? ws + w.recv_lse : ws + w.send_lse;
-    // 3. combine the W partials of this rank's rows
+    if (world > 1) {  // the combine waits for the exchange
+        if (hipError_t he = hipEventRecord(c->ev[0], c->xstream)) return hip_fail(he, "hipEventRecord");
+        if (hipError_t he = hipStreamWaitEvent(s, c->ev[0], 0)) return hip_fail(he, "hipStreamWaitEvent");
+    }
+    // combine the W partials of this rank's rows
     void* rows_out = gather && world > 1 ? (void*)(ws + w.gather + rank * (size_t)BH * Lc * d * esize(dtype)) : o;
-    if (int st = fa_combine(ro, rl, rows_out, world, B, H, Lc, d, dtype, partial_dtype, stream))
+    if (int st = fa_combine(ws + w.recv_o, ws + w.recv_lse, rows_out, world, B, H, Lc, d, dtype, partial_dtype,
+                            stream))
         return core_fail(st, "fa_combine");
     if (!gather || world == 1) return ok();
-    // 4. all-gather [W][B*H][Lc][d] then the strided copy to [B*H][W*Lc][d]
+    // all-gather [W][B*H][Lc][d] then the strided copy to [B*H][W*Lc][d]
     const size_t part = (size_t)BH * Lc * d * esize(dtype);
-    if (ncclResult_t r = ncclAllGather(ws + w.gather + rank * part, ws + w.gather, part, ncclUint8,
-                                       (ncclComm_t)comm, s))
+    if (ncclResult_t r = ncclAllGather(ws + w.gather + rank * part, ws + w.gather, part, ncclUint8, c->nccl, s))
         return rccl_fail(r, "ncclAllGather");
     const size_t row_bytes = (size_t)Lc * d * esize(dtype);
     for (int p = 0; p < world; ++p)
         if (hipError_t he = hipMemcpy2DAsync((char*)o + p * row_bytes, (size_t)L * d * esize(dtype),
                                              ws + w.gather + p * part, row_bytes, row_bytes, BH,
                                              hipMemcpyDeviceToDevice, s))
-            return fail(FA_ERR_HIP, "gather copy: %s", hipGetErrorString(he));
+            return hip_fail(he, "gather copy");
     return ok();
 }
 

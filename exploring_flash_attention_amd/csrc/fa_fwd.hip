@@ -12,7 +12,7 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
-    if (a.Lk % bk_for(D) || !(FA_NOTAIL_MASK & d_bit(D)))
+    if (a.Lk % bk_for(D) || !(kNoTailMask & d_bit(D)))
         hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads),
                            lds, s, a);
     else
@@ -34,7 +34,6 @@ static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
 
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s) {
     if (a.strided) return launch_fwd_strided(t, pt, d, mode, a, s);
-    if (FA_W64 && mode == kFinal && d == 128) return launch_fwd_w64(t, a, s);
     if (mode == kFinal) {
         if (t == Elem::BF16) return launch_d<__bf16, __bf16, kFinal>(d, a, s);
         if (t == Elem::F16) return launch_d<_Float16, _Float16, kFinal>(d, a, s);

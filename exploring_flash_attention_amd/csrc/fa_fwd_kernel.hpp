@@ -36,131 +36,30 @@
 
 #include "fa_device.hpp"
 
-// Build knobs for A/B experiments (scripts/build_variants.sh, scripts/ab.py); the
-// defaults are the measured-best settings.  FA_ABL_* are ablations (wrong results,
-// timing only) used to attribute time to the kernel's phases.
-#ifndef FA_WIDE_STORE
-#define FA_WIDE_STORE 1
-#endif
-// FA_MFMA_ROWSUM: the softmax denominator as one more MFMA column block (ones . P^T)
-// instead of 32 VALU adds per tile: sums the same 16-bit-rounded P the numerator uses.
-// Default off: -4 % at d=128, within noise at d=32 (A/B).
-#ifndef FA_MFMA_ROWSUM_MAXD
-#define FA_MFMA_ROWSUM_MAXD 0
-#endif
-// FA_ROWSUM16_MASK (head-dim bits): the softmax denominator on v_mfma_f32_16x16x32 instead of
-// VALU adds: A = a 0/1 pattern, B = each packed P^T fragment as it is, so one MFMA per
-// 16-key fragment sums both key halves of 16 query rows into 4 accumulator registers
-// (lane l ends up holding the sum of query row (l & 15) + 16 * (l >> 5)); sums the same
-// 16-bit-rounded P the numerator uses
-// (at d = 32 the final no-tail contiguous kernel only; elsewhere every mode, key tails and
-// strided tensors alike, so that a strided view gives the contiguous result bit for bit.  A/B: C2 +3.5 %, C3 +1.2 %,
-// L = 2048 +1.3 %, L = 1000 (key tail) +1.3 %, d = 64 +1.7 %, the C5 partial kernel +1.4 %,
-// the fused split 0; errors equal or lower.  The d = 32 kernel is held to 128 registers and
-// d = 64 to 168 -- four / three waves per SIMD, as without it -- and they and d = 128 spill a
-// few registers after the KV loop, none inside it; the other d = 32 instantiations would)
-#ifndef FA_ROWSUM16_MASK
-#define FA_ROWSUM16_MASK 7
-#endif
-#ifndef FA_DMA_LATE
-#define FA_DMA_LATE 1
-#endif
-#ifndef FA_PRIO
-#define FA_PRIO 0
-#endif
-// a sched_barrier between the P.V MFMAs and the next tile's mask + row max, per head dim
-// (bitmask as FA_UNIFORM_WID): after the v_maximum3 change it costs C3 0.7-1.2 %, C4 1-1.6 %
-// (without it hipcc interleaves the row max with the last P.V MFMAs), C2 / d=64 0, and still
-// pays 1.7 % at d=256
-#ifndef FA_ROWMAX_FENCE
-#define FA_ROWMAX_FENCE 0x8
-#endif
-// FA_SGB: explicit sched_group_barrier pattern for the steady step (1: QK phase 16 x {MFMA,
-// 1 LDS read, 5 VALU}, PV phase 16 x {MFMA, 2 LDS reads, 3 VALU}; 2: 4 / 4 VALU)
-#ifndef FA_SGB
-#define FA_SGB 0
-#endif
-// FA_IGLP: __builtin_amdgcn_iglp_opt(FA_IGLP - 1) in the steady step (0 = none)
-#ifndef FA_IGLP
-#define FA_IGLP 0
-#endif
-#ifndef FA_ABL_NODMAWAIT
-#define FA_ABL_NODMAWAIT 0
-#endif
-#ifndef FA_ABL_NOBAR
-#define FA_ABL_NOBAR 0
-#endif
-#ifndef FA_ABL_NOEXP
-#define FA_ABL_NOEXP 0
-#endif
-#ifndef FA_ABL_NODMA
-#define FA_ABL_NODMA 0
-#endif
-#ifndef FA_ABL_NOPV
-#define FA_ABL_NOPV 0
-#endif
-#ifndef FA_ABL_NOQK
-#define FA_ABL_NOQK 0
-#endif
-// readfirstlane wave id (the DMA's M0 values become SGPR arithmetic): a bitmask over
-// d = 32/64/128/256 (bits 0..3).  A/B with the no-tail step: d=32 +3 %, d=64 0, d=128 -1.7 %.
-#ifndef FA_UNIFORM_WID
-#define FA_UNIFORM_WID 1
-#endif
-// the no-tail specialisation (TAIL = false) per d, same bitmask: d=32 +1.6 %, d=128 +0.5 %,
-// d=64 -7 % (hipcc's schedule of the single-block step is worse there)
-#ifndef FA_NOTAIL_MASK
-#define FA_NOTAIL_MASK 0xD
-#endif
-constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
-constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
-    return (FA_ROWSUM16_MASK & d_bit(d)) != 0 && (d > 32 || (mode == 0 && !tail && !strided));
-}
-// launch bound (waves per SIMD) of an instantiation: the RS16 kernels keep the occupancy the
-// VALU-sum kernels reach (d = 32: four, d = 64: three)
-constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
-    return rs16_on(d, mode, tail, strided) && d <= 32 ? 4 : rs16_on(d, mode, tail, strided) && d == 64 ? 3 : fa::waves_per_simd(d);
-}
-
-// FA_PP: the d = 128 final no-tail kernel as a ping-pong of two 4-wave groups in one 8-wave
-// workgroup (build with -DFA_WAVES=8; see the PP loop)
-#ifndef FA_PP
-#define FA_PP 0
-#endif
-// FA_PP_PRIO: static s_setprio 1 for ping-pong group A (1) or B (2) through the loop
-#ifndef FA_PP_PRIO
-#define FA_PP_PRIO 0
-#endif
-#ifndef FA_RSRC32
-#define FA_RSRC32 1
-#endif
-// row max on v_maximum3_f32 (no canonicalising v_max x,x per MFMA result)
-#ifndef FA_MAXNC
-#define FA_MAXNC 1
-#endif
-// packed fp32 softmax arithmetic for d <= FA_PK_MAXD (0 = off)
-// FA_QSCALE_MASK (head-dim bits, d_bit): Q pre-scaled by c = log2(e) * scale once per
-// workgroup (rounded to the input type) and -m splatted into the QK^T accumulators'
-// initial value, so the exponent needs no per-score FMA
-#ifndef FA_QSCALE_MASK
-#define FA_QSCALE_MASK 0  // off: +2-4 % but peaked rows lose accuracy
-#endif
-// FA_QSPLIT_MASK (head-dim bits; 16-bit brain-float inputs only): QSCALE with c*Q split into
-// two bf16 terms (hi + lo: ~16 significant bits, so peaked rows keep their accuracy) and -m
-// entered by one more MFMA per 32-key block (A = ones in k = 0..2, B = -m as three bf16
-// terms) instead of a splat of -m into the accumulators
-#ifndef FA_QSPLIT_MASK
-#define FA_QSPLIT_MASK 0
-#endif
-// FA_PK_SPLIT: in the packed exponent path, a 32-key block's FMAs all ahead of its
-// exponentials (hipcc otherwise puts each v_exp_f32 right behind the v_pk_fma_f32 that feeds
-// it, one hazard s_nop each): C2 +2 %, bitwise-equal outputs
-#ifndef FA_PK_SPLIT
-#define FA_PK_SPLIT 1
-#endif
-#ifndef FA_PK_MAXD
-#define FA_PK_MAXD 32  // A/B: d=32 +2.4 %, d=64 -4 %
-#endif
+// Per-head-dim tuning, fixed at the measured-best settings (A/B in one process, DESIGN.md
+// section 5; the experiment builds that produced them are in git history, not in the product):
+//  * row sums on v_mfma_f32_16x16x32 (A = a 0/1 pattern, B = each packed P^T fragment as it
+//    is, so one MFMA per 16-key fragment sums both key halves of 16 query rows into 4
+//    accumulator registers; lane l ends up with the sum of query row (l & 15) + 16 * (l >> 5))
+//    at every d; at d = 32 only in the final no-tail contiguous kernel (the other d = 32
+//    instantiations would spill inside the loop under their register bound).  C2 +3.5 %,
+//    C3 +1.2 %, d = 64 +1.7 %, the C5 partial kernel +1.4 %; sums the same 16-bit-rounded P
+//    the numerator uses;
+//  * a scheduling fence between the P.V MFMAs and the next tile's row max at d = 256 (+1.7 %;
+//    0 or negative elsewhere);
+//  * the DMA's M0 destinations from an SGPR wave id at d = 32 (+3 %; d = 128 -1.7 %);
+//  * the no-tail step specialisation at d = 32 / 128 / 256 (d = 64: -7 %);
+//  * packed fp32 exponent arithmetic at d = 32 (C2 +2.4 %; d = 64 -4 %), its FMAs of a 32-key
+//    block issued ahead of the block's exponentials (+2 %).
+constexpr int kRowmaxFenceMask = 0x8;  // d = 256
+constexpr int kUniformWidMask = 0x1;   // d = 32
+constexpr int kNoTailMask = 0xD;       // d = 32, 128, 256
+constexpr int kPackedMaxD = 32;
+// (the row-sum MFMA table, rs16_on, and the launch bounds, kernel_wps, live in
+// fa_internal.hpp: the host's split planner sizes its grids with the same occupancy)
+static_assert(fa::kernel_wps(32, 0, false, false) == 4 && fa::kernel_wps(64, 2, true, false) == 3 &&
+                  fa::kernel_wps(128, 0, false, false) == 2 && fa::kernel_wps(256, 0, false, false) == 1,
+              "occupancy table");
 
 // FA_STAMPS (diagnostic builds only): wave 0 of every workgroup writes s_memtime stamps at
 // the phase boundaries into g_fa_stamps (never into an output), read back through
@@ -216,11 +115,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     // bounded by 2^kThr instead of 1.  kThr = 8 measurably loses accuracy on peaked rows
     // (the dominant p is no longer exactly 1.0 in bf16), 4 does not (tests).
     constexpr float kThr = 4.f;
-    constexpr bool QSPLIT = (FA_QSPLIT_MASK & d_bit(D)) != 0 && std::is_same_v<T, __bf16>;
-    constexpr bool QSCALE = (FA_QSCALE_MASK & d_bit(D)) != 0 || QSPLIT;
-    constexpr bool FA_MFMA_ROWSUM = D <= FA_MFMA_ROWSUM_MAXD;
-    constexpr bool RS16 = rs16_on(D, MODE, TAIL, STRIDED) && !FA_MFMA_ROWSUM;
-    constexpr bool PP = FA_PP && MODE == kFinal && !TAIL && !STRIDED && D == 128 && kWaves == 8 && !QSCALE;
+    constexpr bool RS16 = rs16_on(D, MODE, TAIL, STRIDED);
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: K ring (2 slots) then V ring (2 slots), one [kBK][D] tile image per slot.
@@ -235,9 +130,9 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    // wave-uniform and PROVABLY so (an SGPR): the LDS-DMA destinations (M0) derived from it
-    // then need no v_readfirstlane per DMA, and no VGPRs hold per-piece LDS addresses
-    const int wid = (FA_UNIFORM_WID & d_bit(D)) ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+    // wave-uniform and, where it pays, PROVABLY so (an SGPR): the LDS-DMA destinations (M0)
+    // derived from it then need no v_readfirstlane per DMA
+    const int wid = (kUniformWidMask & d_bit(D)) ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int l32 = lane & 31;
     const int hf = lane >> 5;
 
@@ -256,8 +151,6 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     const int64_t hb = STRIDED ? bh / a.H : 0, hh = STRIDED ? bh - hb * a.H : 0;
     const int64_t q_head = STRIDED ? hb * a.q_stride[0] + hh * a.q_stride[1] : bh * a.Lq * D;
     const int64_t k_head = STRIDED ? hb * a.k_stride[0] + hh * a.k_stride[1] : bh * a.Lk * D;
-    // Buffer descriptors: K/V cover exactly this split's keys, so the DMA of the last
-    // (partial) tile reads zeros past kv_end with no clamping code.
     // Q descriptor over this workgroup's query tile only, so that its 32-bit offsets stay
     // small however long the sequence (rows past Lq read zeros)
     const int64_t q_tile0 = (int64_t)qt * kBQ;
@@ -303,7 +196,6 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
         // descriptor over exactly the tile's valid keys (32-bit scalar arithmetic)
         // (readfirstlane: hipcc evaluates the clamp with v_med3, and a descriptor word it
         // cannot prove uniform turns every buffer op into a waterfall loop -- T20)
-#if FA_RSRC32
         const int rem = nkv - t * kBK;
         const int valid = TAIL ? __builtin_amdgcn_readfirstlane(rem < kBK ? (rem > 0 ? rem : 0) : kBK)
                                : (t < ntiles ? kBK : 0);
@@ -311,12 +203,6 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
         const int bytes = STRIDED ? (valid > 0 ? (valid - 1) * krb + ROWB : 0) : valid * ROWB;
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc32((const char*)base + (int64_t)t * (STRIDED ? (int64_t)kBK * krb : (int64_t)TILEB), bytes);
-#else
-        const int64_t off = (int64_t)t * TILEB;
-        const int64_t kv_bytes = (int64_t)nkv * ROWB;
-        const __amdgpu_buffer_rsrc_t rs =
-            make_rsrc((const char*)base + off, kv_bytes > off ? kv_bytes - off : 0);
-#endif
         if (NDMA >= kWaves || dma_wave) {
 #pragma unroll
             for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], 0);
@@ -334,10 +220,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 #pragma unroll
         for (int db = 0; db < NDB; ++db) o[r][db] = f32x16{};
     float m[RB], l[RB];  // reference max (log2 units) and this lane's half of the row sum
-    f32x16 lsum[RB];     // FA_MFMA_ROWSUM: every register = the row sum of the lane's query
-#pragma unroll
-    for (int r = 0; r < RB; ++r) lsum[r] = f32x16{};
-    f32x4 ls16[RB];  // RS16: row sum of query (lane & 15) + 16 * (lane >> 5), in every register
+    f32x4 ls16[RB];      // RS16: row sum of query (lane & 15) + 16 * (lane >> 5), in every register
 #pragma unroll
     for (int r = 0; r < RB; ++r) ls16[r] = f32x4{};
     // A of the RS16 MFMA: output rows 0-7 sum lane groups 0 and 2 (query n, both key halves),
@@ -347,38 +230,12 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     for (int j = 0; j < 8; ++j) sel16[j] = static_cast<T>(((lane & 15) < 8) == (((lane >> 4) & 1) == 0) ? 1.f : 0.f);
     const int rs16_src = ((lane & 31) < 16 ? (lane & 31) : (lane & 31) + 16) * 4;  // holder of own row
     const int rs16_row = ((lane & 15) + 16 * (lane >> 5)) * 4;                      // row held here
-    v8 ones;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ones[j] = static_cast<T>(1.0f);
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-        m[r] = QSCALE ? 0.f : -INFINITY;  // QSCALE: the accumulators start at -m = 0
+        m[r] = -INFINITY;
         l[r] = 0.f;
     }
     const float c = a.scale_log2;
-    // QSPLIT: the low bf16 term of c*Q, and the bias MFMA's operands (-m as hi + mid + lo)
-    v8 qlo[RB][QSPLIT ? NKS : 1];
-    v8 bias_a, bias_b[RB];
-    auto set_bias = [&](int r) {
-        const float nm = -m[r];
-        const T h = static_cast<T>(nm);
-        const float r1 = nm - static_cast<float>(h);
-        const T mid = static_cast<T>(r1);
-        const T lo = static_cast<T>(r1 - static_cast<float>(mid));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bias_b[r][j] = static_cast<T>(0.f);
-        if (hf == 0) {
-            bias_b[r][0] = h;
-            bias_b[r][1] = mid;
-            bias_b[r][2] = lo;
-        }
-    };
-    if constexpr (QSPLIT) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bias_a[j] = static_cast<T>(hf == 0 && j < 3 ? 1.f : 0.f);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) set_bias(r);
-    }
 
     // S^T[key][q] = K . Q^T for one tile (two 32-key blocks), every K fragment feeding the
     // RB row blocks.  Fragments are read in groups of two k-steps, one group ahead.
@@ -395,19 +252,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 #pragma unroll
         for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2) {
-                if constexpr (QSPLIT) {
-                    s[r][b2] = f32x16{};
-                } else if constexpr (QSCALE) {
-                    const float nm = -m[r];
-                    const double nm2 = __builtin_bit_cast(double, f32x2{nm, nm});
-                    typedef double d8 __attribute__((ext_vector_type(8)));
-                    const d8 v = {nm2, nm2, nm2, nm2, nm2, nm2, nm2, nm2};
-                    s[r][b2] = __builtin_bit_cast(f32x16, v);
-                } else {
-                    s[r][b2] = f32x16{};
-                }
-            }
+            for (int b2 = 0; b2 < NKB; ++b2) s[r][b2] = f32x16{};
         rd(0, kf[0]);
 #pragma unroll
         for (int g = 0; g < NKS / G; ++g) {
@@ -417,59 +262,35 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 #pragma unroll
                 for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
-                    for (int r = 0; r < RB; ++r) {
-#if FA_ABL_NOQK
-                        asm volatile("" ::"v"(kf[g & 1][b2][j]));
-                        s[r][b2][j] += (float)qf[r][g * G + j][0];
-#else
-                        s[r][b2] = M::mma(kf[g & 1][b2][j], qf[r][g * G + j], s[r][b2]);
-                        if constexpr (QSPLIT) s[r][b2] = M::mma(kf[g & 1][b2][j], qlo[r][g * G + j], s[r][b2]);
-#endif
-                    }
-        }
-        if constexpr (QSPLIT) {
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int r = 0; r < RB; ++r) s[r][b2] = M::mma(bias_a, bias_b[r], s[r][b2]);
+                    for (int r = 0; r < RB; ++r) s[r][b2] = M::mma(kf[g & 1][b2][j], qf[r][g * G + j], s[r][b2]);
         }
     };
-    // P = 2^(S*c - m) in place, and its row sum into l
+    // P = 2^(S*c - m) in place, and (VALU-sum kernels) its row sum into l
     auto exp_tile = [&](f32x16 (&s)[RB][NKB]) {
-        if constexpr (D <= FA_PK_MAXD && !FA_MFMA_ROWSUM && RS16) {
+        if constexpr (D <= kPackedMaxD && RS16) {
+            // packed fp32 FMAs (the MFMA pipe is mostly idle at small d), all FMAs of a 32-key
+            // block ahead of its exponentials: no exponential right behind the FMA that feeds
+            // it (a hazard wait state each)
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
                 const f32x2 c2 = {c, c}, nm2 = {-m[r], -m[r]};
 #pragma unroll
                 for (int b2 = 0; b2 < NKB; ++b2) {
-                    if constexpr (FA_PK_SPLIT && !QSCALE) {
-                        // all FMAs of the block first: no exponential right behind the FMA
-                        // that feeds it (a hazard wait state each)
-#pragma unroll
-                        for (int i = 0; i < 16; i += 2) {
-                            f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
-                            x = __builtin_elementwise_fma(x, c2, nm2);
-                            s[r][b2][i] = x[0];
-                            s[r][b2][i + 1] = x[1];
-                        }
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) s[r][b2][i] = __builtin_amdgcn_exp2f(s[r][b2][i]);
-                        continue;
-                    }
 #pragma unroll
                     for (int i = 0; i < 16; i += 2) {
                         f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
-                        if constexpr (!QSCALE) x = __builtin_elementwise_fma(x, c2, nm2);
-                        s[r][b2][i] = __builtin_amdgcn_exp2f(x[0]);
-                        s[r][b2][i + 1] = __builtin_amdgcn_exp2f(x[1]);
+                        x = __builtin_elementwise_fma(x, c2, nm2);
+                        s[r][b2][i] = x[0];
+                        s[r][b2][i + 1] = x[1];
                     }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) s[r][b2][i] = __builtin_amdgcn_exp2f(s[r][b2][i]);
                 }
             }
             return;
         }
-        if constexpr (D <= FA_PK_MAXD && !FA_MFMA_ROWSUM) {
-            // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU instruction where
-            // the MFMA pipe is mostly idle (small d is VALU-bound)
+        if constexpr (D <= kPackedMaxD) {
+            // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU instruction
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
                 const f32x2 c2 = {c, c}, nm2 = {-m[r], -m[r]};
@@ -479,7 +300,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 #pragma unroll
                     for (int i = 0; i < 16; i += 2) {
                         f32x2 x = {s[r][b2][i], s[r][b2][i + 1]};
-                        if constexpr (!QSCALE) x = __builtin_elementwise_fma(x, c2, nm2);
+                        x = __builtin_elementwise_fma(x, c2, nm2);
                         x[0] = __builtin_amdgcn_exp2f(x[0]);
                         x[1] = __builtin_amdgcn_exp2f(x[1]);
                         s[r][b2][i] = x[0];
@@ -498,14 +319,10 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-#if FA_ABL_NOEXP
-                    s[r][b2][i] = __builtin_fmaf(s[r][b2][i], c, -m[r]);
-#else
-                    s[r][b2][i] = __builtin_amdgcn_exp2f(QSCALE ? s[r][b2][i] : __builtin_fmaf(s[r][b2][i], c, -m[r]));
-#endif
-                    if (!FA_MFMA_ROWSUM && !RS16) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
+                    s[r][b2][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r][b2][i], c, -m[r]));
+                    if (!RS16) sum4[(b2 * 16 + i) & 3] += s[r][b2][i];
                 }
-            if (!FA_MFMA_ROWSUM && !RS16) l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
+            if (!RS16) l[r] += (sum4[0] + sum4[1]) + (sum4[2] + sum4[3]);
         }
     };
     // keys past the end of the split (only in the last, partial tile) -> -inf
@@ -524,7 +341,8 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
                 }
         }
     };
-    // row max of a (masked) tile, both lane halves, in log2 units
+    // row max of a (masked) tile, both lane halves, in log2 units (v_maximum3: no
+    // canonicalising v_max x,x per MFMA result, unlike fmaxf)
     auto rowmax = [&](const f32x16 (&s)[RB][NKB], float (&mx)[RB]) {
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
@@ -535,10 +353,8 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             for (int b2 = 0; b2 < NKB; ++b2)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
-                    if (b2 > 0 || i >= 4) mx4[i & 3] = FA_MAXNC ? fmax_nc(mx4[i & 3], s[r][b2][i]) : fmaxf(mx4[i & 3], s[r][b2][i]);
-            // (QSCALE: already in log2 units, relative to m)
-            mx[r] = FA_MAXNC ? pair_max(fmax_nc(fmax_nc(mx4[0], mx4[1]), fmax_nc(mx4[2], mx4[3]))) * (QSCALE ? 1.f : c)
-                             : pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * (QSCALE ? 1.f : c);
+                    if (b2 > 0 || i >= 4) mx4[i & 3] = fmax_nc(mx4[i & 3], s[r][b2][i]);
+            mx[r] = pair_max(fmax_nc(fmax_nc(mx4[0], mx4[1]), fmax_nc(mx4[2], mx4[3]))) * c;
         }
     };
     // V^T fragments of (32-key block b2, 32-column block db): 4 transposed reads of 4
@@ -570,8 +386,8 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     };
 
     // One pipeline step for tile t, whose raw (masked) scores are in sc and row max in mx:
-    //   DMA K(t+2), V(t+1) into the ring slots freed by the previous step's barrier;
-    //   rescale decision; QK^T(t+1) -> sn beside exp / sum of sc; pack P;
+    //   rescale decision; DMA K(t+2), V(t+1) into the ring slots freed by the previous step's
+    //   barrier; QK^T(t+1) -> sn beside exp / sum of sc; pack P;
     //   P.V(t), then mask + row max of sn;  barrier (which also drains the DMA).
     // P = t & 1 is a compile-time constant (the loop runs steps in pairs).
     auto step = [&](auto par_c, auto flags_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
@@ -586,54 +402,25 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
         //   DMAK      tile t+2 exists (its K is prefetched now)
         constexpr int F = decltype(flags_c)::value;
         constexpr bool MORE = F & 1, MASKNEXT = TAIL && (F & 2), DMAK = F & 4;
-#if !FA_DMA_LATE
-        if (!FA_ABL_NODMA && t + 2 < ntiles) dma_tile(kbase, kring + P * TILEB, t + 2);
-        if (!FA_ABL_NODMA && t + 1 < ntiles) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
-#endif
 
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          if constexpr (QSCALE) {
-            // scores (sc, mx) are relative to m (set from tile 0 in the prologue)
-            if (__builtin_amdgcn_ballot_w64(mx[r] > kThr)) {
-                const float delta = fmaxf(mx[r], 0.f);
-                const float alpha = __builtin_amdgcn_exp2f(-delta);
-                m[r] += delta;
-                if constexpr (QSPLIT) set_bias(r);
-                l[r] *= alpha;
-                if constexpr (RS16)
-                    ls16[r] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
-#pragma unroll
-                for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) sc[r][b2][i] -= delta;
-#pragma unroll
-                for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
-            }
-          } else {
             if (__builtin_amdgcn_ballot_w64(mx[r] > m[r] + kThr)) {
                 const float m_new = fmaxf(m[r], mx[r]);
                 const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
                 m[r] = m_new;
                 l[r] *= alpha;
-                if (FA_MFMA_ROWSUM) lsum[r] *= alpha;
                 if constexpr (RS16)
                     ls16[r] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
 #pragma unroll
                 for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
             }
-          }
         }
 
-#if FA_DMA_LATE
         // DMA issued in the MFMA block (the scheduler spreads the pieces among the MFMAs);
         // tile counts are checked against the compile-time MORE where possible
-        if constexpr (!FA_ABL_NODMA && DMAK) dma_tile(kbase, kring + P * TILEB, t + 2);
-        if constexpr (!FA_ABL_NODMA && MORE) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
-#endif
-#if FA_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
+        if constexpr (DMAK) dma_tile(kbase, kring + P * TILEB, t + 2);
+        if constexpr (MORE) dma_tile(vbase, vring + (1 - P) * TILEB, t + 1);
         if constexpr (MORE) qk(kring + (1 - P) * TILEB, sn);
         exp_tile(sc);
         v8 pb[RB][NKB][2];
@@ -665,12 +452,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
                 const u32x4 vv = {vcur[ss][0][0], vcur[ss][0][1], vcur[ss][1][0], vcur[ss][1][1]};
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {
-#if FA_ABL_NOPV
-                    asm volatile("" ::"v"(vv), "v"(pb[r][B2][ss]));
-#else
                     o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
-#endif
-                    if (FA_MFMA_ROWSUM && DB == 0) lsum[r] = M::mma(ones, pb[r][B2][ss], lsum[r]);
                     if constexpr (RS16 && DB == 0) ls16[r] = M::mma16(sel16, pb[r][B2][ss], ls16[r]);
                 }
             }
@@ -684,125 +466,11 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             }
         });
         if constexpr (MORE) {
-            if constexpr ((FA_ROWMAX_FENCE & d_bit(D)) != 0) __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((kRowmaxFenceMask & d_bit(D)) != 0) __builtin_amdgcn_sched_barrier(0);
             if constexpr (MASKNEXT) mask(t + 1, sn);
             rowmax(sn, mx);
         }
-#if FA_SGB
-        if constexpr (MORE && NKB * NDB * 2 == 16 && NKB * NKS == 16) {
-            constexpr int VQ = FA_SGB == 1 ? 5 : 4, VP = FA_SGB == 1 ? 3 : 4;
-            static_for<16>([&](auto) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, VQ, 0);
-            });
-            static_for<16>([&](auto) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, VP, 0);
-            });
-        }
-#endif
-#if FA_IGLP
-        if constexpr (MORE) __builtin_amdgcn_iglp_opt(FA_IGLP - 1);
-#endif
-#if FA_ABL_NOBAR
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#elif FA_ABL_NODMAWAIT
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#else
-#if FA_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
-#endif
-    };
-
-    // ---- ping-pong halves (PP): the step split at the P.V boundary.  Group A (waves 0-3)
-    // runs H1(0) H2(0) H1(1) ...; group B (waves 4-7, one per SIMD beside an A wave) runs the
-    // same sequence one half-step later, so that on every SIMD one wave's QK^T + exponentials
-    // share the issue port with the other's P.V + row max.  One barrier per half-step; the
-    // DMA of global half-step h (2 pieces per wave) lands by the barrier ending h+1:
-    //   h = 2s: K(s+2) -> K slot s&1      h = 2s+1: V(s+1) -> V slot (s+1)&1
-    // (A: H1(t) issues K(t+2), H2(t) V(t+1); B: H1(t) V(t+1), H2(t) K(t+3)).  Each slot's
-    // previous tile was last read two barriers earlier, so two-slot rings suffice.
-    // (steady loop: this half-step's 2 pieces stay in flight; the tail, whose code hipcc may
-    // spill around -- scratch ops count in vmcnt too -- drains everything)
-    auto pp_bar = [&](auto drain_c) {
-        static_assert(!PP || DPW == 2, "ping-pong waits count two DMA pieces per half-step");
-        // (sched_barriers: hipcc would otherwise sink register-only work such as MFMAs across it)
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (decltype(drain_c)::value)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto half1 = [&](auto par_c, auto more_c, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
-                     const float (&mx)[RB], v8 (&pb)[RB][NKB][2], auto dma) {
-        constexpr int P = decltype(par_c)::value;
-        constexpr bool MORE = decltype(more_c)::value;
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            if (__builtin_amdgcn_ballot_w64(mx[r] > m[r] + kThr)) {
-                const float m_new = fmaxf(m[r], mx[r]);
-                const float alpha = __builtin_amdgcn_exp2f(m[r] - m_new);
-                m[r] = m_new;
-                l[r] *= alpha;
-                if constexpr (RS16)
-                    ls16[r] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
-#pragma unroll
-                for (int db = 0; db < NDB; ++db) o[r][db] *= alpha;
-            }
-        }
-        dma();
-        if constexpr (MORE) qk(kring + (1 - P) * TILEB, sn);
-        exp_tile(sc);
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    u32x4 u;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        u[j] = pack2<T>(sc[r][b2][8 * ss + 2 * j], sc[r][b2][8 * ss + 2 * j + 1]);
-                    pb[r][b2][ss] = __builtin_bit_cast(v8, u);
-                }
-    };
-    auto half2 = [&](auto par_c, auto more_c, f32x16 (&sn)[RB][NKB], float (&mx)[RB],
-                     const v8 (&pb)[RB][NKB][2], auto dma) {
-        constexpr bool MORE = decltype(more_c)::value;
-        dma();
-        u32x2 vcur[2][2], vnext[2][2];
-        read_v(par_c, std::integral_constant<int, 0>{}, vcur, vbase0, vbase1);
-        vwait(vcur);
-        static_for<NKB * NDB>([&](auto i_c) {
-            constexpr int I = decltype(i_c)::value;
-            constexpr int B2 = I / NDB, DB = I % NDB;
-            if constexpr (I + 1 < NKB * NDB)
-                read_v(par_c, std::integral_constant<int, I + 1>{}, vnext, vbase0, vbase1);
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                const u32x4 vv = {vcur[ss][0][0], vcur[ss][0][1], vcur[ss][1][0], vcur[ss][1][1]};
-#pragma unroll
-                for (int r = 0; r < RB; ++r) {
-                    o[r][DB] = M::mma(__builtin_bit_cast(v8, vv), pb[r][B2][ss], o[r][DB]);
-                    if constexpr (RS16 && DB == 0) ls16[r] = M::mma16(sel16, pb[r][B2][ss], ls16[r]);
-                }
-            }
-            if constexpr (I + 1 < NKB * NDB) {
-                vwait(vnext);
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    vcur[ss][0] = vnext[ss][0];
-                    vcur[ss][1] = vnext[ss][1];
-                }
-            }
-        });
-        if constexpr (MORE) rowmax(sn, mx);
     };
 
     // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
@@ -815,19 +483,6 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[r][ks]));
-    if constexpr (QSCALE) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float x = static_cast<float>(qf[r][ks][j]) * c;
-                    qf[r][ks][j] = static_cast<T>(x);
-                    if constexpr (QSPLIT) qlo[r][ks][j] = static_cast<T>(x - static_cast<float>(qf[r][ks][j]));
-                }
-        }
-    }
     __syncthreads();
     FA_STAMP(1);
     f32x16 sa[RB][NKB], sb[RB][NKB];
@@ -835,84 +490,10 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     qk(kring, sa);
     if constexpr (TAIL) mask(0, sa);
     rowmax(sa, mx);
-    if constexpr (QSCALE) {  // m = tile 0's row max; its scores relative to it
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            m[r] = mx[r];
-            if constexpr (QSPLIT) set_bias(r);
-#pragma unroll
-            for (int b2 = 0; b2 < NKB; ++b2)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) sa[r][b2][i] -= mx[r];
-            mx[r] = 0.f;
-        }
-    }
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
     FA_STAMP(2);
 
-    if constexpr (PP) {
-        using C0 = std::integral_constant<int, 0>;
-        using C1 = std::integral_constant<int, 1>;
-        using Y = std::integral_constant<bool, true>;
-        using N = std::integral_constant<bool, false>;
-        auto run = [&](auto g_c) {
-            constexpr int G = decltype(g_c)::value;  // 0: group A, 1: group B (half a step behind)
-            v8 pb[RB][NKB][2];
-            auto dk = [&](int t, auto slot_c) { dma_tile(kbase, kring + decltype(slot_c)::value * TILEB, t); };
-            auto dv = [&](int t, auto slot_c) { dma_tile(vbase, vring + decltype(slot_c)::value * TILEB, t); };
-            // H1(t) / H2(t) with t's parity P and this group's DMA share
-            auto h1 = [&](auto par_c, auto more_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB]) {
-                constexpr int P = decltype(par_c)::value;
-                half1(par_c, more_c, sc, sn, mx, pb, [&] {
-                    if constexpr (G == 0) dk(t + 2, std::integral_constant<int, P>{});
-                    else dv(t + 1, std::integral_constant<int, 1 - P>{});
-                });
-            };
-            auto h2 = [&](auto par_c, auto more_c, int t, f32x16 (&sn)[RB][NKB]) {
-                constexpr int P = decltype(par_c)::value;
-                half2(par_c, more_c, sn, mx, pb, [&] {
-                    if constexpr (G == 0) dv(t + 1, std::integral_constant<int, 1 - P>{});
-                    else dk(t + 3, std::integral_constant<int, 1 - P>{});
-                });
-            };
-            if constexpr (FA_PP_PRIO == G + 1) __builtin_amdgcn_s_setprio(1);
-            if constexpr (G == 1) {
-                dk(2, C0{});
-                pp_bar(Y{});
-            }
-            int t = 0;
-            for (; t + 2 < ntiles; t += 2) {
-                h1(C0{}, Y{}, t, sa, sb);
-                pp_bar(N{});
-                h2(C0{}, Y{}, t, sb);
-                pp_bar(N{});
-                h1(C1{}, Y{}, t + 1, sb, sa);
-                pp_bar(N{});
-                h2(C1{}, Y{}, t + 1, sa);
-                pp_bar(N{});
-            }
-            if (ntiles - t == 2) {
-                h1(C0{}, Y{}, t, sa, sb);
-                pp_bar(Y{});
-                h2(C0{}, Y{}, t, sb);
-                pp_bar(Y{});
-                h1(C1{}, N{}, t + 1, sb, sa);
-                pp_bar(Y{});
-                h2(C1{}, N{}, t + 1, sa);
-            } else {
-                h1(C0{}, N{}, t, sa, sb);
-                pp_bar(Y{});
-                h2(C0{}, N{}, t, sb);
-            }
-            // A's last barrier pairs with B's after its last H1; B ends without one.  Every
-            // DMA (including the zero-filled ones past the last tile) lands before the exit.
-            if constexpr (G == 0) pp_bar(Y{});
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr (FA_PP_PRIO == G + 1) __builtin_amdgcn_s_setprio(0);
-        };
-        if (__builtin_amdgcn_readfirstlane(tid >> 8)) run(std::integral_constant<int, 1>{});
-        else run(std::integral_constant<int, 0>{});
-    } else {
+    {
         using C0 = std::integral_constant<int, 0>;
         using C1 = std::integral_constant<int, 1>;
         // flags: 1 = MORE, 2 = MASKNEXT, 4 = DMAK (see step)
@@ -941,13 +522,11 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     const int64_t o_head = STRIDED ? hb * a.o_stride[0] + hh * a.o_stride[1] : bh * a.Lq * D;
     const int64_t orow = STRIDED ? a.o_stride[2] : D;
     // ---- epilogue: lane holds O^T[dv][q_row] for dv = 32*db + (i&3) + 8*(i>>2) + 4*hf
-    // store v * scale as one 16-bit output row (row base Oh)
+    // store v * scale as one 16-bit output row (row base Oh).  Column groups g and g+1 of a
+    // row sit in lanes l (cols 8g..+3, 8g+8..+11) and l+32 (8g+4..+7, 8g+12..+15); one
+    // v_permlane32_swap per dword leaves 16 contiguous bytes in each lane -> one dwordx4
+    // store per pair instead of two dwordx2 (cdna_hip_programming.md T21).
     auto store_row = [&](unsigned short* Oh, const f32x16 (&v)[NDB], float scale) {
-#if FA_WIDE_STORE
-        // Column groups g and g+1 of a row sit in lanes l (cols 8g..+3, 8g+8..+11) and
-        // l+32 (8g+4..+7, 8g+12..+15); one v_permlane32_swap per dword leaves 16
-        // contiguous bytes in each lane -> one dwordx4 store per pair instead of two
-        // dwordx2 (cdna_hip_programming.md T21).
 #pragma unroll
         for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -961,19 +540,11 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
                 const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
                 *(u32x4*)(Oh + db * 32 + 8 * gp + 8 * hf) = u;
             }
-#else
-#pragma unroll
-        for (int db = 0; db < NDB; ++db)
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                u32x2 u;
-                u[0] = pack2<T>(v[db][4 * g4 + 0] * scale, v[db][4 * g4 + 1] * scale);
-                u[1] = pack2<T>(v[db][4 * g4 + 2] * scale, v[db][4 * g4 + 3] * scale);
-                *(u32x2*)(Oh + db * 32 + 8 * g4 + 4 * hf) = u;
-            }
-#endif
     };
-
+    auto row_sum = [&](int r) {
+        return RS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_src, __builtin_bit_cast(int, ls16[r][0])))
+                    : pair_sum(l[r]);
+    };
     if constexpr (MODE == kFused) {
         // Split-KV partials combined on chip.  Every workgroup stores its normalised partial
         // O (PT) and lse in FRAGMENT order -- lane-linear 16-byte pieces, so both the stores
@@ -1006,9 +577,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
-                const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0]
-                            : RS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_src, __builtin_bit_cast(int, ls16[r][0])))
-                                   : pair_sum(l[r]);
+                const float l_tot = row_sum(r);
                 inv[r] = 1.f / l_tot;
                 lse_own[r] = m[r] + __builtin_amdgcn_logf(l_tot);
                 esc_own[r] = 0.f;
@@ -1153,9 +722,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         const int64_t q_row = q_row0 + 32 * r;
-        const float l_tot = FA_MFMA_ROWSUM ? lsum[r][0]
-                            : RS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_src, __builtin_bit_cast(int, ls16[r][0])))
-                                   : pair_sum(l[r]);
+        const float l_tot = row_sum(r);
         float inv = 1.f / l_tot;
         if (q_row >= a.Lq) continue;
         if constexpr (MODE == kFinal) {

@@ -7,44 +7,33 @@
 
 namespace fa {
 
-// Keys per KV tile and query rows per wave of the forward kernel.  A wave owns kRB
-// blocks of 32 query rows (one 32x32x16 MFMA column block each) and every K / V
-// fragment it reads from LDS feeds kRB MFMAs; a workgroup has kWaves waves.
-//   kRB = 1: 32 rows per wave, <= 256 registers, two waves per SIMD (default);
-//   kRB = 2: 64 rows per wave, ~460 registers, ONE wave per SIMD -- halves the LDS
-//            fragment traffic per MFMA, but hipcc's schedule for it (AGPR shuffling, no
-//            second wave to hide latency) measured 1.6x slower at C3 (profiles/).
-#ifndef FA_WAVES
-#define FA_WAVES 4
-#endif
-#ifndef FA_RB
-#define FA_RB 1
-#endif
-// Keys per KV tile, per head dim (a multiple of 32).  Small d has registers to spare and
-// is bound by per-tile overheads, so it takes longer tiles.
-#ifndef FA_BK32
-#define FA_BK32 (FA_RB == 1 ? 64 : 32)
-#endif
-#ifndef FA_BK64
-#define FA_BK64 (FA_RB == 1 ? 64 : 32)
-#endif
-#ifndef FA_BK128
-#define FA_BK128 (FA_RB == 1 ? 64 : 32)
-#endif
-#ifndef FA_BK256
-#define FA_BK256 32
-#endif
-constexpr int bk_for(int d) {
-    return d <= 32 ? FA_BK32 : d <= 64 ? FA_BK64 : d <= 128 ? FA_BK128 : FA_BK256;
-}
-constexpr int kRB = FA_RB;
+// Geometry of the forward kernel: a wave owns one block of 32 query rows (one 32x32x16 MFMA
+// column block), a workgroup 4 waves = 128 rows, KV tiles of 64 keys (32 at d = 256).
+// (64 rows per wave -- one wave per SIMD, every K / V fragment feeding two MFMAs -- and 8-wave
+// workgroups were measured slower; they live in git history.)
+constexpr int bk_for(int d) { return d <= 128 ? 64 : 32; }
+constexpr int kRB = 1;
 constexpr int kRowsPerWave = 32 * kRB;
-constexpr int kWaves = FA_WAVES;
+constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * 64;
 constexpr int kBQ = kWaves * kRowsPerWave;
-constexpr int kWavesPerSimd = kRB == 1 ? 2 : 1;  // occupancy the register budget is sized for
-// d = 256 holds 64 Q and 128 O registers per lane: one wave per SIMD, AGPRs in use
-constexpr int waves_per_simd(int d) { return d > 128 ? 1 : kWavesPerSimd; }
+// waves per SIMD the register budget is sized for (d = 256 holds 64 Q and 128 O registers
+// per lane: one wave per SIMD)
+constexpr int waves_per_simd(int d) { return d > 128 ? 1 : 2; }
+// Row sums on the 16x16x32 MFMA (fa_fwd_kernel.hpp) at d = 32 / 64 / 128; at d = 32 only in
+// the final no-tail contiguous kernel.  Those kernels are held to the occupancy the VALU-sum
+// kernels reach (d = 32: four waves per SIMD, d = 64: three); kernel_wps = the launch bound
+// of an instantiation = workgroups per CU (4 waves per workgroup, one per SIMD).
+constexpr int d_bit(int d) { return d == 32 ? 1 : d == 64 ? 2 : d == 128 ? 4 : 8; }
+constexpr int kRowsum16Mask = 0x7;
+constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
+    return (kRowsum16Mask & d_bit(d)) != 0 && (d > 32 || (mode == 0 && !tail && !strided));
+}
+constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
+    return rs16_on(d, mode, tail, strided) && d <= 32 ? 4
+           : rs16_on(d, mode, tail, strided) && d == 64 ? 3
+                                                        : waves_per_simd(d);
+}
 
 enum class Elem : int { F16 = 0, BF16 = 1, F32 = 2, F64 = 3, F16S = 4 };
 // F16S (split-KV partials only): fp16 values scaled per row by a power of two 2^-e so that the
@@ -108,12 +97,6 @@ hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStrea
 // the strided instantiations (fa_fwd_strided.hip); launch_fwd forwards there when a.strided
 hipError_t launch_fwd_strided(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
-// d = 128 final mode with 64 rows per wave (fa_fwd_w64.hip); FA_W64 selects it
-#ifndef FA_W64
-#define FA_W64 0  // measured: steady state equal to fa_fwd_kernel, per-item seam 1.5x
-#endif
-hipError_t launch_fwd_w64(Elem t, const FwdArgs& a, hipStream_t s);
-int w64_rows_per_block();
 // fp64 mode (fa_fwd64.hip): 64 query rows x 16-key tiles; final or row-layout partial
 hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s);

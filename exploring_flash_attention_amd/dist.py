@@ -50,6 +50,35 @@ def shard_bounds(L, world, rank):
     return rank * n, (rank + 1) * n
 
 
+def _peer(group, r):
+    return dist.get_global_rank(group, r) if group is not None else r
+
+
+def _chunk_ops(o_send, lse_send, o_recv, lse_recv, group, rank, world, s):
+    """Step s of the shifted exchange: send chunk rank+s to rank+s, receive chunk rank from
+    rank-s (every step a perfect matching: all ranks' links busy at once)."""
+    dst, src = (rank + s) % world, (rank - s) % world
+    return [dist.P2POp(dist.isend, o_send[dst], _peer(group, dst), group),
+            dist.P2POp(dist.irecv, o_recv[src], _peer(group, src), group),
+            dist.P2POp(dist.isend, lse_send[dst], _peer(group, dst), group),
+            dist.P2POp(dist.irecv, lse_recv[src], _peer(group, src), group)]
+
+
+def exchange_partials(o_send, lse_send, o_recv, lse_recv, group=None):
+    """The exchange step alone, on partials already computed in the send layout
+    ([W][B*H][L/W][d] and their lse): chunk j goes to rank j over W-1 shifted send/recv steps
+    posted together; the own chunk is copied locally (it never crosses a link).  Returns the
+    RCCL works (wait() them, or let the stream order the next kernel).  bench.py times it to
+    report the xGMI exchange separately from the kernels."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    ops_ = []
+    for s in range(1, world):
+        ops_ += _chunk_ops(o_send, lse_send, o_recv, lse_recv, group, rank, world, s)
+    o_recv[rank].copy_(o_send[rank])
+    lse_recv[rank].copy_(lse_send[rank])
+    return dist.batch_isend_irecv(ops_) if ops_ else []
+
+
 def _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc):
     """Steps 1-2 pipelined: the partials are computed one destination chunk at a time, and
     chunk j is handed to RCCL (send to rank j, matched receive from the rank sending to us)
@@ -67,25 +96,24 @@ def _exchange_overlapped(q, k_shard, v_shard, group, partial_dtype, world, Lc):
     lse_send = torch.empty((world, B * H, Lc) + ((2,) if scaled else ()), dtype=lse_dtype, device=q.device)
     o_recv, lse_recv = torch.empty_like(o_send), torch.empty_like(lse_send)
 
-    def peer(r):
-        return dist.get_global_rank(group, r) if group is not None else r
-
     works = []
     for s in range(1, world):
-        dst, src = (rank + s) % world, (rank - s) % world
+        dst = (rank + s) % world
         _partial_chunk_fn(q[:, :, dst * Lc:(dst + 1) * Lc], k_shard, v_shard, o_send[dst], lse_send[dst],
                           partial_dtype)
-        works += dist.batch_isend_irecv([
-            dist.P2POp(dist.isend, o_send[dst], peer(dst), group),
-            dist.P2POp(dist.irecv, o_recv[src], peer(src), group),
-            dist.P2POp(dist.isend, lse_send[dst], peer(dst), group),
-            dist.P2POp(dist.irecv, lse_recv[src], peer(src), group),
-        ])
+        works += dist.batch_isend_irecv(_chunk_ops(o_send, lse_send, o_recv, lse_recv, group, rank, world, s))
     _partial_chunk_fn(q[:, :, rank * Lc:(rank + 1) * Lc], k_shard, v_shard, o_recv[rank], lse_recv[rank],
                       partial_dtype)
     for w in works:
         w.wait()
     return o_recv, lse_recv
+
+
+def _uses_rccl(group):
+    """True when the group moves device tensors over RCCL: its backend is "nccl", or a
+    mixed-backend group ("cpu:gloo,cuda:nccl") whose device half is."""
+    b = str(dist.get_backend(group))
+    return b == "nccl" or "cuda:nccl" in b
 
 
 def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=None,
@@ -107,7 +135,7 @@ def splitkv_attention(q, k_shard, v_shard, group=None, partial_dtype=None,
     if L % world:
         raise ValueError(f"L={L} must be divisible by world size {world}")
     Lc = L // world
-    if world > 1 and overlap and q.is_cuda and dist.get_backend(group) != "nccl":
+    if world > 1 and overlap and q.is_cuda and not _uses_rccl(group):
         # gloo's send/recv take host memory only (its all_to_all / all_gather stage device
         # tensors): device tensors on a non-RCCL group take the all-to-all path
         overlap = False

@@ -19,8 +19,8 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import (FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP16_SCALED, FA_DTYPE_FP32, FA_DTYPE_FP64,
-                   FA_KV_TILES_AUTO, check, lib)
+from ._lib import (FA_BLOCKS_PER_WG_AUTO, FA_DTYPE_BF16, FA_DTYPE_FP16, FA_DTYPE_FP16_SCALED, FA_DTYPE_FP32,
+                   FA_DTYPE_FP64, FA_KV_TILES_AUTO, check, lib)
 
 # torch.float64 runs the fp64 kernels (the reference's USE_FP64 build): fp64 MFMA, softmax,
 # partials and lse -- the bit-tight mode, not the fast one
@@ -172,15 +172,6 @@ def attention_v1(q, k, v, out=None):
     return _unpad_into(op, o, d)
 
 
-def attention_v1_w64(q, k, v, out=None):
-    """FA-v1 forward on the experimental 64-rows-per-wave kernel (d = 128 only)."""
-    _check_qkv(q, k, v)
-    o = _out(out, q)
-    B, H, L, d = q.shape
-    check(lib().fa_fwd_v1_w64(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
-    return o
-
-
 def _d_tiles(d, d_tile_qk, d_tile_v):
     """d tiles default to min(32, d) (the reference's D_TILE = 32 where d allows it)."""
     return (min(32, d) if d_tile_qk is None else int(d_tile_qk),
@@ -212,8 +203,15 @@ def _kvtpb(kv_tiles_per_block):
     return FA_KV_TILES_AUTO if kv_tiles_per_block == "auto" else int(kv_tiles_per_block)
 
 
+def _bpw(blocks_per_workgroup):
+    g = FA_BLOCKS_PER_WG_AUTO if blocks_per_workgroup is None else int(blocks_per_workgroup)
+    if g < 0:
+        raise ValueError(f"blocks_per_workgroup={g} must be >= 1 (or None for the library's grouping)")
+    return g
+
+
 def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
-                       partial_dtype=None):
+                       partial_dtype=None, blocks_per_workgroup=None):
     """(bytes, num_splits) of the split-KV workspace: num_splits = the reference's key blocks;
     the bytes cover the partials actually combined through the workspace (v2_split_plan) in
     partial_dtype (per-row scaled fp16 by default; fp64 for fp64 inputs)."""
@@ -222,29 +220,34 @@ def v2_workspace_bytes(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16,
     nbytes = ctypes.c_size_t()
     ns = ctypes.c_int()
     d = kernel_head_dim(d)
-    check(lib().fa_fwd_v2_workspace_size(B, H, L, d, int(kv_tiles_per_block), _DTYPES[dtype],
-                                         _PDTYPES[pd], ctypes.byref(nbytes), ctypes.byref(ns)))
+    check(lib().fa_fwd_v2_workspace_size_ex(B, H, L, d, int(kv_tiles_per_block), _bpw(blocks_per_workgroup),
+                                            _DTYPES[dtype], _PDTYPES[pd], ctypes.byref(nbytes), ctypes.byref(ns)))
     return nbytes.value, ns.value
 
 
-def v2_split_plan(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16):
+def v2_split_plan(B, H, L, d, kv_tiles_per_block=4, dtype=torch.bfloat16, blocks_per_workgroup=None):
     """(key_blocks, blocks_per_workgroup, partials_per_tile) of fa_fwd_v2's schedule: the
     reference's key blocks of kv_tiles_per_block tiles, how many consecutive blocks one
     workgroup combines on chip, and how many partial workgroups per query tile are combined
-    through the workspace."""
+    through the workspace.  ``blocks_per_workgroup`` None: the library's grouping; n >= 1 fixes
+    it (1 = one workgroup and one HBM partial per key block, the reference's layout)."""
     kb, g, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    check(lib().fa_fwd_v2_split_plan(B, H, L, kernel_head_dim(d), int(_kvtpb(kv_tiles_per_block)), _DTYPES[dtype],
+    check(lib().fa_fwd_v2_split_plan(B, H, L, kernel_head_dim(d), int(_kvtpb(kv_tiles_per_block)),
+                                     _bpw(blocks_per_workgroup), _DTYPES[dtype],
                                      ctypes.byref(kb), ctypes.byref(g), ctypes.byref(p)))
     return kb.value, g.value, p.value
 
 
 def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, partial_dtype=None,
-                 out=None, workspace=None):
+                 out=None, workspace=None, blocks_per_workgroup=None):
     """FA-v2 split-KV forward (partial kernel + combine kernel).
 
     A split is ``kv_tiles_per_block`` KV tiles of the kernel's own tile size (64 keys;
     32 at d = 256); ``kv_tiles_per_block="auto"`` lets the library pick the split from the
     device's occupancy (no split when the query tiles already fill the GPU).
+    ``blocks_per_workgroup`` (None: the library's grouping, v2_split_plan) fixes how many
+    consecutive key blocks one workgroup combines on chip; 1 is the reference's layout (one
+    HBM partial per key block).
     Partial outputs are kept as per-row scaled fp16 by default (``PARTIAL_FP16_SCALED``: half
     the workspace traffic of ``torch.float32``, 11 significant bits relative to each row's
     largest partial, no fp16 range limit); ``torch.float32`` or the input dtype on request.
@@ -262,33 +265,30 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
     if st is False:
         return _via_contiguous(attention_v2, q, k, v, o, kv_tiles_per_block=kv_tiles_per_block,
                                d_tile_qk=d_tile_qk, d_tile_v=d_tile_v, partial_dtype=partial_dtype,
-                               workspace=workspace)
+                               workspace=workspace, blocks_per_workgroup=blocks_per_workgroup)
     pd = _default_pdtype(q.dtype, partial_dtype, fused=True)
     kv_tiles_per_block = _kvtpb(kv_tiles_per_block)
-    nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd)
+    bpw = _bpw(blocks_per_workgroup)
+    nbytes, _ = v2_workspace_bytes(B, H, L, d, kv_tiles_per_block, q.dtype, pd, bpw)
     if workspace is None:
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=q.device)
     elif workspace.numel() * workspace.element_size() < nbytes:
         raise ValueError(f"workspace too small: {nbytes} bytes needed")
     wsb = workspace.numel() * workspace.element_size()
-    if D == d and st is None:
-        check(lib().fa_fwd_v2(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
-                              int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb,
-                              _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
-        return o
     if D == d:
+        sq, skv, so = (None, None, None) if st is None else st
         check(lib().fa_fwd_v2_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
-                                 int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb, st[0], st[1],
-                                 st[2], 1.0 / d ** 0.5, _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
+                                 int(d_tile_v), int(kv_tiles_per_block), bpw, _ptr(workspace), wsb, sq, skv,
+                                 so, 1.0 / d ** 0.5, _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
         return o
     for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
         if not 0 < int(t) <= d:
             raise _lib.FaArgumentError(1, f"{name}={int(t)} must satisfy 0 < {name} <= d={d}")
     qp, kp, vp = (_pad_d(t, D) for t in (q, k, v))
     op = torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
-    check(lib().fa_fwd_v2_scaled(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, int(d_tile_qk),
-                                 int(d_tile_v), int(kv_tiles_per_block), _ptr(workspace), wsb, 1.0 / d ** 0.5,
-                                 _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
+    check(lib().fa_fwd_v2_ex(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, int(d_tile_qk),
+                             int(d_tile_v), int(kv_tiles_per_block), bpw, _ptr(workspace), wsb, None, None, None,
+                             1.0 / d ** 0.5, _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
     return _unpad_into(op, o, d)
 
 

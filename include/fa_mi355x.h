@@ -127,12 +127,9 @@ int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o,
  * made automatic). */
 #define FA_KV_TILES_AUTO (-1)
 
-/* Experimental: the FA-v1 forward at d = 128 (bf16 / fp16) on the 64-rows-per-wave kernel
- * (csrc/fa_fwd_w64.hip: one wave per SIMD, MFMA state in asm-owned AGPRs, persistent
- * workgroups).  Same arguments and results as fa_fwd_v1; kept for measurement
- * ("64-row waves"): fa_fwd_v1 uses it only when built with -DFA_W64=1. */
-int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o,
-                  int64_t B, int64_t H, int64_t L, int64_t d, int dtype, void* stream);
+/* blocks_per_workgroup value that lets the library group the key blocks of a query tile onto
+ * workgroups itself (fa_fwd_v2_split_plan). */
+#define FA_BLOCKS_PER_WG_AUTO 0
 
 /* Bytes of device workspace fa_fwd_v2 needs for this problem.  A split (the reference's key
  * block) is kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
@@ -142,15 +139,23 @@ int fa_fwd_v1_w64(const void* q, const void* k, const void* v, void* o,
 int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d,
                              int kv_tiles_per_block, int dtype, int partial_dtype,
                              size_t* bytes, int* num_splits);
+/* fa_fwd_v2_workspace_size for fa_fwd_v2_ex's blocks_per_workgroup (FA_BLOCKS_PER_WG_AUTO:
+ * the library's grouping, as fa_fwd_v2_workspace_size). */
+int fa_fwd_v2_workspace_size_ex(int64_t B, int64_t H, int64_t L, int64_t d,
+                                int kv_tiles_per_block, int blocks_per_workgroup,
+                                int dtype, int partial_dtype, size_t* bytes, int* num_splits);
 
 /* How fa_fwd_v2 schedules the key blocks of a query tile: *key_blocks = ceil(L / (kv_tiles_per_block
- * * bk)) (the reference's partials), *blocks_per_workgroup consecutive blocks per workgroup
+ * * bk)) (the reference's partials), *blocks_per_wg_out consecutive blocks per workgroup
  * (combined on chip: the online softmax carried across them), *partials_per_tile partial
- * workgroups per query tile (combined through the workspace).  Blocks are grouped as long as
- * >= 4 workgroups per resident slot remain; FA_SPLIT_GROUP=<n> in the environment fixes the
- * group size (1: one workgroup and one HBM partial per key block).  Any pointer may be NULL. */
+ * workgroups per query tile (combined through the workspace).  With blocks_per_workgroup =
+ * FA_BLOCKS_PER_WG_AUTO blocks are grouped as long as >= 4 workgroups per resident slot remain;
+ * a positive value fixes the group size (1: one workgroup and one HBM partial per key block, the
+ * reference's layout; clamped to the number of blocks).  The plan depends only on the
+ * arguments and the device's compute-unit count.  Any output pointer may be NULL. */
 int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block,
-                         int dtype, int* key_blocks, int* blocks_per_workgroup, int* partials_per_tile);
+                         int blocks_per_workgroup, int dtype, int* key_blocks,
+                         int* blocks_per_wg_out, int* partials_per_tile);
 
 /* FA-v2 split-KV forward: one workgroup per (q-tile, group of key blocks, b*h) computes its
  * keys' normalised partial O and log-sum-exp into the workspace; the last workgroup of each
@@ -171,10 +176,12 @@ int fa_fwd_v2_scaled(const void* q, const void* k, const void* v, void* o,
                      int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
                      void* workspace, size_t workspace_bytes, double softmax_scale,
                      int dtype, int partial_dtype, void* stream);
-/* fa_fwd_v2_scaled on strided q, k, v, o (strides as for fa_fwd_v1_ex). */
+/* fa_fwd_v2_scaled on strided q, k, v, o (strides as for fa_fwd_v1_ex), with an explicit key-block
+ * grouping (blocks_per_workgroup as for fa_fwd_v2_split_plan; FA_BLOCKS_PER_WG_AUTO = the
+ * library's); the workspace is sized by fa_fwd_v2_workspace_size_ex with the same value. */
 int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o,
                  int64_t B, int64_t H, int64_t L, int64_t d,
-                 int d_tile_qk, int d_tile_v, int kv_tiles_per_block,
+                 int d_tile_qk, int d_tile_v, int kv_tiles_per_block, int blocks_per_workgroup,
                  void* workspace, size_t workspace_bytes,
                  const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
                  double softmax_scale, int dtype, int partial_dtype, void* stream);

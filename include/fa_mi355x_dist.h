@@ -6,12 +6,17 @@
  * d_tile_v,kv_tiles_per_block), flash_attention_v2/CUDA/flash_attention_v2.h:438, whose
  * partial_attention_kernel (:243) and reduction_kernel (:356) become, per rank:
  *
- *   1. fa_fwd_partial over the rank's key shard, for ALL L query rows, written in the
- *      all-to-all send layout [W][B*H][L/W][d] (+ lse [W][B*H][L/W]);
- *   2. one grouped RCCL send/recv round: chunk p goes to rank p, so every rank receives the
- *      W partials of its own L/W query rows -- all xGMI links busy at once, where a ring
- *      reduce-scatter would serialise on one link per step;
- *   3. fa_combine of the W received partials -> the rank's rows [B, H, L/W, d] of O;
+ *   1. the partial kernel (fa_fwd_partial_ex) over the rank's key shard, one launch per
+ *      destination chunk of query rows (chunk p = the rows rank p will own), written in the
+ *      send layout [W][B*H][L/W][d] (+ lse [W][B*H][L/W]);
+ *   2. as soon as chunk p is queued, one RCCL send/recv step on the communicator's own
+ *      stream: step s sends chunk rank+s to rank+s and receives chunk rank from rank-s -- a
+ *      shifted exchange, every step a perfect matching (all xGMI links busy at once, where a
+ *      ring reduce-scatter would serialise on one link per step) -- so the transfer of one
+ *      chunk overlaps the next chunk's kernel; the rank's own chunk is computed last, straight
+ *      into the receive buffer (it never crosses a link);
+ *   3. fa_combine of the W partials -> the rank's rows [B, H, L/W, d] of O, once the exchange
+ *      stream has finished (an event, no host wait);
  *   4. optionally an RCCL all-gather (+ a strided copy) -> the full [B, H, L, d] O.
  *
  * One process per GPU.  Kept in its own library so that processes that never shard (and
@@ -38,7 +43,9 @@ const char* fa_dist_last_error(void);
 /* Rank 0 creates the communicator id; the caller ships its 128 bytes to every rank. */
 int fa_dist_get_unique_id(void* id);
 
-/* Collective over all `world` ranks (each on its own device, set current beforehand). */
+/* Collective over all `world` ranks (each on its own device, set current beforehand).  The
+ * handle owns the RCCL communicator plus the exchange stream and events the forward uses, all
+ * created here so that fa_fwd_v2_dist itself never allocates. */
 int fa_dist_comm_init(void** comm, int world, int rank, const void* id);
 int fa_dist_comm_destroy(void* comm);
 
@@ -52,7 +59,11 @@ int fa_fwd_v2_dist_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, in
 /* q: [B, H, L, d] (identical on every rank); k_shard, v_shard: this rank's keys
  * [B, H, L/W, d] (rank r holds keys [r*L/W, (r+1)*L/W)); o: this rank's query rows
  * [B, H, L/W, d] of O, or the full [B, H, L, d] O when gather != 0.  Asynchronous on
- * `stream` (RCCL runs on the same stream). */
+ * `stream`: the kernels and the all-gather run on it, the send/recv steps on the handle's
+ * exchange stream, ordered against it by events.  Every argument is checked before anything
+ * is enqueued (a call that returns an error has posted nothing to the peers); the one failure
+ * that can still strike part-way -- an RCCL enqueue error after earlier steps were posted --
+ * returns FA_ERR_RCCL and marks the handle unusable (later calls refuse; destroy it). */
 int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void* o,
                    int64_t B, int64_t H, int64_t L, int64_t d, void* comm, int gather,
                    void* workspace, size_t workspace_bytes, int dtype, int partial_dtype,

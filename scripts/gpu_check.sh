@@ -20,7 +20,7 @@ for s in $STEPS; do
       echo "smoke rc=$rc"; tail -5 $OUT/smoke.log; stop_if_crash $rc smoke
       [ $rc -eq 0 ] || exit 1 ;;
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS:--x} > $OUT/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ${PYTEST_ARGS:--x} > $OUT/pytest_gpu.log 2>&1; rc=$?
       echo "pytest rc=$rc"; tail -25 $OUT/pytest_gpu.log; stop_if_crash $rc tests ;;
     bench)
       timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err; rc=$?

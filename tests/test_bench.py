@@ -32,3 +32,56 @@ def test_sample_heads_and_host_cores():
     usable, total = bench.host_cores()
     assert 1 <= usable <= total == os.cpu_count()
     assert bench.cpu_model()
+
+
+def test_gpus_request_beyond_the_node_fails_loudly():
+    """`bench.py --gpus 2` with no launcher on a node with fewer GPUs (this container has none)
+    exits non-zero with a message -- never a one-GPU line labelled n_gpus 1."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.strip() == "" and "--gpus 2 requested" in r.stderr
+
+
+def test_world_size_disagreeing_with_gpus_is_an_error():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2 and "disagree" in r.stderr and r.stdout.strip() == ""
+
+
+def test_spawn_ranks_starts_n_ranks_and_propagates_failure(tmp_path):
+    """The launcher bench.py uses for --gpus N: N processes with RANK / WORLD_SIZE set, and a
+    failing rank makes the whole launch fail (non-zero status)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, sys\n"
+        "r, w = os.environ['RANK'], os.environ['WORLD_SIZE']\n"
+        "open(os.path.join(sys.argv[1], 'rank' + r), 'w').write(w)\n"
+        "sys.exit(7 if sys.argv[2] == r else 0)\n")
+    assert bench.spawn_ranks(3, str(script), [str(tmp_path), "-1"]) == 0
+    assert sorted(p.name for p in tmp_path.glob("rank[0-9]")) == ["rank0", "rank1", "rank2"]
+    assert all((tmp_path / f"rank{i}").read_text() == "3" for i in range(3))
+    for p in tmp_path.glob("rank[0-9]"):
+        p.unlink()
+    assert bench.spawn_ranks(2, str(script), [str(tmp_path), "1"]) != 0
+
+
+def test_extra_shapes_split_where_the_library_splits():
+    """The split-KV bench extras: the two low-parallelism shapes are planned with more than one
+    partial per query tile by the library (on the MI355X's 256 CUs), their `unsplit` twins
+    with one."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from exploring_flash_attention_amd import ops
+    shapes = {s[0]: s for s in bench.EXTRA_SHAPES}
+    for base, ppt in (("b2h2_l16k", 4), ("b1h2_l16k", 8)):
+        _, B, H, L, d, _, kvt, grp = shapes[base + "_splitkv"]
+        assert grp is None and ops.v2_split_plan(B, H, L, d, kvt)[2] == ppt
+        _, B, H, L, d, _, kvt, grp = shapes[base + "_unsplit"]
+        blocks = ops.v2_split_plan(B, H, L, d, kvt)[0]
+        assert grp == "all" and ops.v2_split_plan(B, H, L, d, kvt, blocks_per_workgroup=blocks)[2] == 1

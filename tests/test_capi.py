@@ -125,25 +125,36 @@ def test_workspace_size_and_v2_checks():
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
     assert ns.value == 16 and nbytes.value == 256
     kb, g, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
+    AUTO = L.FA_BLOCKS_PER_WG_AUTO
+    assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, AUTO, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
                                     ctypes.byref(p)) == 0
     assert (kb.value, g.value, p.value) == (16, 16, 1)
-    # FA_SPLIT_GROUP=1: one workgroup and one HBM partial per key block (the reference's layout)
-    os.environ["FA_SPLIT_GROUP"] = "1"
+    # blocks_per_workgroup = 1: one workgroup and one HBM partial per key block (the reference's
+    # layout), fixed by an argument -- the same call gives the same plan whatever the environment
+    os.environ["FA_SPLIT_GROUP"] = "7"  # (round 2's environment knob: must be ignored now)
     try:
-        assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, L.FA_DTYPE_BF16,
-                                            ctypes.byref(nbytes), ctypes.byref(ns)) == 0
-        assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+        assert lib.fa_fwd_v2_workspace_size_ex(32, 8, 4096, 128, 4, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_BF16,
+                                               ctypes.byref(nbytes), ctypes.byref(ns)) == 0
+        assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, 1, L.FA_DTYPE_BF16, None, ctypes.byref(g),
                                         ctypes.byref(p)) == 0
+        assert (g.value, p.value) == (1, 16)
+        n_auto = ctypes.c_size_t()
+        assert lib.fa_fwd_v2_workspace_size(32, 8, 4096, 128, 4, L.FA_DTYPE_BF16, L.FA_DTYPE_BF16,
+                                            ctypes.byref(n_auto), None) == 0
+        assert n_auto.value == 256
     finally:
         del os.environ["FA_SPLIT_GROUP"]
-    assert (g.value, p.value) == (1, 16)
+    # a group larger than the block count is clamped; negative is refused
+    assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, 99, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                    ctypes.byref(p)) == 0 and (g.value, p.value) == (16, 1)
+    assert lib.fa_fwd_v2_split_plan(32, 8, 4096, 128, 4, -1, L.FA_DTYPE_BF16, None, None,
+                                    None) == L.FA_ERR_INVALID_ARG
     rows = 16 * 32 * 8 * 4096
     # partial O + lse (fragment order, 128-row tiles: 4096 = 32 x 128) + one counter per tile
     assert nbytes.value == rows * 128 * 2 + rows * 4 + 32 * 8 * 32 * 4
     assert nbytes.value > 2 ** 32  # 64-bit sizes (the reference overflows int32 here)
     # a short batch of long sequences: one workgroup per key block
-    assert lib.fa_fwd_v2_split_plan(1, 1, 8192, 128, 4, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
+    assert lib.fa_fwd_v2_split_plan(1, 1, 8192, 128, 4, AUTO, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
                                     ctypes.byref(p)) == 0
     assert (kb.value, g.value, p.value) == (32, 1, 32)
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
@@ -207,23 +218,19 @@ def test_split_grid_bound():
     FA_ERR_UNSUPPORTED (never truncated to 32 bits), before any launch."""
     lib = L.lib()
     nbytes, ns = ctypes.c_size_t(), ctypes.c_int()
-    # B*H = 2^16, L = 2^20, one workgroup per key block (FA_SPLIT_GROUP=1):
+    # B*H = 2^16, L = 2^20, one workgroup per key block (blocks_per_workgroup = 1):
     # 8192 query tiles x 16384 one-tile splits x 65536 heads
-    os.environ["FA_SPLIT_GROUP"] = "1"
-    try:
-        st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
-                                          ctypes.byref(nbytes), ctypes.byref(ns))
-        assert st == L.FA_ERR_UNSUPPORTED and b"2^31-1" in lib.fa_last_error()
-        fake = ctypes.c_void_p(0x10000)
-        st = lib.fa_fwd_v2(fake, fake, fake, fake, 256, 256, 1 << 20, 64, 32, 32, 1, fake, 1 << 40,
-                           L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
-        assert st == L.FA_ERR_UNSUPPORTED
-        # the same shape with long splits fits: 8192 x 1 x 65536 < 2^31
-        st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1 << 14, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
-                                          ctypes.byref(nbytes), ctypes.byref(ns))
-        assert st == 0 and ns.value == 1
-    finally:
-        del os.environ["FA_SPLIT_GROUP"]
+    st = lib.fa_fwd_v2_workspace_size_ex(256, 256, 1 << 20, 64, 1, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                         ctypes.byref(nbytes), ctypes.byref(ns))
+    assert st == L.FA_ERR_UNSUPPORTED and b"2^31-1" in lib.fa_last_error()
+    fake = ctypes.c_void_p(0x10000)
+    st = lib.fa_fwd_v2_ex(fake, fake, fake, fake, 256, 256, 1 << 20, 64, 32, 32, 1, 1, fake, 1 << 40,
+                          None, None, None, 0.125, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32, NULL)
+    assert st == L.FA_ERR_UNSUPPORTED
+    # the same shape with long splits fits: 8192 x 1 x 65536 < 2^31
+    st = lib.fa_fwd_v2_workspace_size_ex(256, 256, 1 << 20, 64, 1 << 14, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
+                                         ctypes.byref(nbytes), ctypes.byref(ns))
+    assert st == 0 and ns.value == 1
     # scheduled normally, the blocks of a query tile share workgroups and the grid fits
     st = lib.fa_fwd_v2_workspace_size(256, 256, 1 << 20, 64, 1, L.FA_DTYPE_BF16, L.FA_DTYPE_FP32,
                                       ctypes.byref(nbytes), ctypes.byref(ns))
@@ -274,11 +281,40 @@ def test_dist_library_exports():
     assert nbytes.value == 2 * (rows * 64 * 4 + rows * 4) + rows * 64 * 2
 
 
-def test_w64_asm_hazard_check():
-    """The inline-asm MFMA kernel passes the static ISA checks (scripts/check_asm_mfma.py)."""
-    import subprocess
-    import sys
-    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "..", "scripts",
-                                                     "check_asm_mfma.py")], capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout + r.stderr
+def test_product_build_carries_no_experiments():
+    """The product library is the shipped kernels only: no experiment or ablation knobs in the
+    kernel sources it is built from, no experimental entry points, and the split schedule
+    depends on arguments only (no environment lookups in the C ABI)."""
+    csrc = os.path.join(ROOT, "exploring_flash_attention_amd", "csrc")
+    mk = open(os.path.join(csrc, "Makefile")).read()
+    srcs = re.search(r"^SRCS\s*=\s*(.*)$", mk, flags=re.M).group(1).split()
+    assert "fa_fwd_w64.hip" not in srcs
+    for f in srcs + ["fa_fwd_kernel.hpp", "fa_device.hpp", "fa_internal.hpp"]:
+        text = open(os.path.join(csrc, f)).read()
+        for knob in ("FA_ABL_", "FA_PP", "FA_SGB", "FA_QSPLIT", "FA_QSCALE", "FA_IGLP", "FA_W64", "getenv"):
+            assert knob not in text, (f, knob)
+    out = os.popen(f"nm -D --defined-only {L.LIB_PATH}").read()
+    assert "fa_fwd_v1_w64" not in out and "fa_fwd_v2_ex" in out
 
+
+def test_dist_argument_and_error_paths():
+    """fa_fwd_v2_dist / fa_dist_comm_* refuse bad arguments before any RCCL or HIP work (CPU:
+    no device, so a communicator cannot be made and says so)."""
+    from exploring_flash_attention_amd import dist as fadist
+    lib = fadist.dist_lib()
+    fake = ctypes.c_void_p(0x10000)
+    st = lib.fa_fwd_v2_dist(fake, fake, fake, fake, 1, 1, 64, 128, None, 0, fake, 1 << 20,
+                            L.FA_DTYPE_BF16, L.FA_DTYPE_FP16_SCALED, None)
+    assert st == L.FA_ERR_INVALID_ARG and b"comm" in lib.fa_dist_last_error()
+    assert lib.fa_dist_get_unique_id(None) == L.FA_ERR_INVALID_ARG
+    comm = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(128)
+    assert lib.fa_dist_comm_init(ctypes.byref(comm), 2, 2, uid) == L.FA_ERR_INVALID_ARG
+    assert lib.fa_dist_comm_init(ctypes.byref(comm), 0, 0, uid) == L.FA_ERR_INVALID_ARG
+    assert lib.fa_dist_comm_init(None, 1, 0, uid) == L.FA_ERR_INVALID_ARG
+    st = lib.fa_dist_comm_init(ctypes.byref(comm), 1, 0, uid)
+    assert st != L.FA_OK and not comm.value  # no device here: an error, never a half-made handle
+    assert lib.fa_dist_comm_destroy(None) == L.FA_OK
+    nbytes = ctypes.c_size_t()
+    assert lib.fa_fwd_v2_dist_workspace_size(1, 1, 64, 128, 2, L.FA_DTYPE_FP64, L.FA_DTYPE_FP32,
+                                             ctypes.byref(nbytes)) == L.FA_ERR_UNSUPPORTED

@@ -6,8 +6,8 @@ flash_attention_v1_tiled_d/CUDA/driver.cu:120-125 and :250, flash_attention_v2/C
 driver.cu:87-90 and :204).  Here:
 
 * C2 / C3 (B32 H8 L1024, d = 32 / 128) and C4 (B32 H8 L4096 d128, KV_TILES_PER_BLOCK = 4:
-  16 splits through the in-kernel combine with scaled fp16 partials, and the automatic
-  split) on N(0,1) bf16 inputs, against the fp64 oracle on 16 sampled heads -- the first
+  as scheduled, and with 16 / 4 partials per query tile through the in-kernel combine with
+  scaled fp16 partials, and the automatic split) on N(0,1) bf16 inputs, against the fp64 oracle on 16 sampled heads -- the first
   and last (b, h) included, every query tile of each, so the 2048-workgroup XCD remap, all
   8 (32 at C4) query tiles of a head and the 16-split combine are all covered;
 * the drivers' own inputs (srand(42) U[-1,1] fp16, oracle_driver_random) at B32 H8 L1024
@@ -57,23 +57,21 @@ def test_fullsize_v1_and_tiled_d(gpu, d):
     _check_sampled(ops.attention_tiled_d(q, k, v, 32, 32), q, k, v)
 
 
-@pytest.mark.parametrize("kvt,group", [(4, None), (4, "1"), (4, "4"), ("auto", None)],
+@pytest.mark.parametrize("kvt,group", [(4, None), (4, 1), (4, 4), ("auto", None)],
                          ids=["kvtpb4", "kvtpb4-one-wg-per-block", "kvtpb4-4-per-wg", "auto"])
-def test_fullsize_c4_splitkv(gpu, kvt, group, monkeypatch):
+def test_fullsize_c4_splitkv(gpu, kvt, group):
     """C4 as scheduled (the 16 key blocks of a query tile on one workgroup), and with
-    FA_SPLIT_GROUP fixing 1 or 4 blocks per workgroup: 16 / 4 partials per query tile
+    blocks_per_workgroup fixing 1 or 4 blocks per workgroup: 16 / 4 partials per query tile
     through the workspace and the in-kernel combine (8192 query tiles)."""
     from exploring_flash_attention_amd import ops
-    if group is not None:
-        monkeypatch.setenv("FA_SPLIT_GROUP", group)
     q, k, v = _device_inputs(4096, 128, seed=4)
-    nbytes, ns = ops.v2_workspace_bytes(B, H, 4096, 128, kvt)
-    blocks, per_wg, partials = ops.v2_split_plan(B, H, 4096, 128, kvt)
+    nbytes, ns = ops.v2_workspace_bytes(B, H, 4096, 128, kvt, blocks_per_workgroup=group)
+    blocks, per_wg, partials = ops.v2_split_plan(B, H, 4096, 128, kvt, blocks_per_workgroup=group)
     if kvt == 4:
         assert ns == blocks == 16 and partials == 16 // int(group or 16)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
-    o1 = ops.attention_v2(q, k, v, kvt, workspace=ws)
-    o2 = ops.attention_v2(q, k, v, kvt, workspace=ws)
+    o1 = ops.attention_v2(q, k, v, kvt, workspace=ws, blocks_per_workgroup=group)
+    o2 = ops.attention_v2(q, k, v, kvt, workspace=ws, blocks_per_workgroup=group)
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)  # the combine order is fixed: bitwise repeatable
     _check_sampled(o1, q, k, v)
@@ -105,31 +103,45 @@ def _driver_metrics(out, ref):
     return float(diff.max()), float((diff[big] / np.abs(ref[big])).max())
 
 
+@pytest.mark.parametrize("group", [None, 1, 2], ids=["as-scheduled", "one-wg-per-block", "2-per-wg"])
 @pytest.mark.parametrize("d", [32, 128])
-def test_driver_compare_full_size(gpu, oracle_lib, d):
+def test_driver_compare_full_size(gpu, oracle_lib, d, group):
+    """The drivers' own inputs and PASS thresholds at B32 H8 L1024 over all 256 heads.  The
+    library schedules L = 1024 with KV_TILES_PER_BLOCK = 4 on the FA-v1 kernel (4 key blocks,
+    one workgroup per query tile); blocks_per_workgroup = 1 / 2 forces the split-KV partials
+    (4 / 2 per query tile) through the workspace and the in-kernel combine, so the v2
+    driver's thresholds cover the combine too."""
     from exploring_flash_attention_amd import ops
     Q, K, V = _driver_inputs(oracle_lib, 1024, d)
     ref = _c_reference(oracle_lib, Q, K, V)
     q, k, v = (torch.from_numpy(x).to(gpu) for x in (Q, K, V))
-    o1 = ops.attention_v1(q, k, v).float().cpu().numpy()
-    ot = ops.attention_tiled_d(q, k, v, 32, 32).float().cpu().numpy()
-    o2 = ops.attention_v2(q, k, v, 4).float().cpu().numpy()
-    ma1, _ = _driver_metrics(o1, ref)
-    mat, _ = _driver_metrics(ot, ref)
+    if group is None:
+        o1 = ops.attention_v1(q, k, v).float().cpu().numpy()
+        ot = ops.attention_tiled_d(q, k, v, 32, 32).float().cpu().numpy()
+        ma1, _ = _driver_metrics(o1, ref)
+        mat, _ = _driver_metrics(ot, ref)
+        assert ma1 < 1e-3, ma1             # flash_attention_v1/CUDA/driver.cu:275
+        assert mat < 1e-2, mat             # flash_attention_v1_tiled_d/CUDA/driver.cu:250
+    _, _, partials = ops.v2_split_plan(B, H, 1024, d, 4, q.dtype, blocks_per_workgroup=group)
+    assert partials == {None: 1, 1: 4, 2: 2}[group]
+    o2 = ops.attention_v2(q, k, v, 4, blocks_per_workgroup=group).float().cpu().numpy()
     ma2, mr2 = _driver_metrics(o2, ref)
-    assert ma1 < 1e-3, ma1             # flash_attention_v1/CUDA/driver.cu:275
-    assert mat < 1e-2, mat             # flash_attention_v1_tiled_d/CUDA/driver.cu:250
     assert ma2 < 0.1 and mr2 < 0.1, (ma2, mr2)  # flash_attention_v2/CUDA/driver.cu:204
     assert ma2 < 1e-3, ma2             # and the stricter v1 bound, which the split path also meets
 
 
-def test_driver_inputs_c4_sampled(gpu, oracle_lib):
-    """C4's shape (L = 4096, 16 splits) on the drivers' generator, against the C oracle on the
-    16 sampled heads (the whole batch would take the C oracle ~30 s)."""
+@pytest.mark.parametrize("group", [None, 1], ids=["as-scheduled", "16-partials"])
+def test_driver_inputs_c4_sampled(gpu, oracle_lib, group):
+    """C4's shape (L = 4096, KV_TILES_PER_BLOCK = 4: 16 key blocks) on the drivers' generator,
+    against the C oracle on the 16 sampled heads (the whole batch would take the C oracle
+    ~30 s): as scheduled (one workgroup per query tile) and with one workgroup per key block
+    (16 partials per query tile through the in-kernel combine)."""
     from exploring_flash_attention_amd import ops
     Q, K, V = _driver_inputs(oracle_lib, 4096, 128)
     q, k, v = (torch.from_numpy(x).to(gpu) for x in (Q, K, V))
-    out = ops.attention_v2(q, k, v, 4).float().cpu().numpy()
+    _, _, partials = ops.v2_split_plan(B, H, 4096, 128, 4, q.dtype, blocks_per_workgroup=group)
+    assert partials == (16 if group == 1 else 1)
+    out = ops.attention_v2(q, k, v, 4, blocks_per_workgroup=group).float().cpu().numpy()
     heads = _sample()
     pick = lambda x: np.stack([x[b, h] for b, h in heads])[None]
     ref = _c_reference(oracle_lib, pick(Q), pick(K), pick(V))

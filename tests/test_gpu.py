@@ -570,17 +570,6 @@ def test_fp64_partial_combine(gpu):
     assert np.abs(o.cpu().numpy() - ref).max() <= 1e-12
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
-def test_w64_kernel(gpu, dtype):
-    """The experimental 64-rows-per-wave kernel (asm-owned AGPRs, persistent workgroups):
-    same gates as fa_fwd_v1, several work items per workgroup, odd and even tile counts."""
-    from exploring_flash_attention_amd import ops
-    for i, (B, H, L) in enumerate(((1, 1, 1), (1, 2, 65), (2, 3, 200), (3, 100, 300), (2, 2, 1024))):
-        q, k, v = _inputs(B, H, L, 128, dtype, seed=40 + i)
-        out = ops.attention_v1_w64(q.to(gpu), k.to(gpu), v.to(gpu))
-        _gate(out, _ref(q, k, v), dtype)
-
-
 def test_scaled_partials_near_bf16_max(gpu):
     """Rows whose output approaches bf16's maximum (|O| ~ 2e38, partial exponent e = 128):
     both combines (in-kernel and fa_combine) weight the splits by 2^(e - E) and apply 2^E
