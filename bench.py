@@ -260,8 +260,9 @@ def c5_breakdown(torch, ops, fdist, dev, world, rank, barrier):
 # Split-KV shapes: C4 itself (KV_TILES_PER_BLOCK = 4) under the library's grouping, with the
 # grouping forced (4 and 1 key blocks per workgroup: 4 / 16 partials per query tile) and the
 # automatic split; and two low-parallelism shapes -- the regime the reference's split-KV exists
-# for (flash_attention_v2/README.md:7-21) -- where the library itself splits, each against the
-# same shape forced onto one workgroup per query tile (blocks_per_workgroup = all blocks).
+# for (flash_attention_v2/README.md:7-21): fewer query tiles than CUs, so the library itself
+# splits (2 and 4 partials per query tile) -- each against the same shape forced onto one
+# workgroup per query tile (blocks_per_workgroup = all blocks).
 EXTRA_SHAPES = (
     # name, B, H, L, d, variant, kv_tiles_per_block, blocks_per_workgroup
     ("c2_fused", 32, 8, 1024, 32, "v1", None, None),
@@ -269,11 +270,12 @@ EXTRA_SHAPES = (
     ("c4_splitkv_4_blocks_per_wg", 32, 8, 4096, 128, "v2", 4, 4),
     ("c4_splitkv_1_block_per_wg", 32, 8, 4096, 128, "v2", 4, 1),
     ("c4_splitkv_auto", 32, 8, 4096, 128, "v2", "auto", None),
-    ("b2h2_l16k_splitkv", 2, 2, 16384, 128, "v2", 4, None),
-    ("b2h2_l16k_unsplit", 2, 2, 16384, 128, "v2", 4, "all"),
-    ("b1h2_l16k_splitkv", 1, 2, 16384, 128, "v2", 4, None),
-    ("b1h2_l16k_unsplit", 1, 2, 16384, 128, "v2", 4, "all"),
+    ("b1h1_l16k_splitkv", 1, 1, 16384, 128, "v2", 4, None),
+    ("b1h1_l16k_unsplit", 1, 1, 16384, 128, "v2", 4, "all"),
+    ("b1h2_l4k_splitkv", 1, 2, 4096, 128, "v2", 4, None),
+    ("b1h2_l4k_unsplit", 1, 2, 4096, 128, "v2", 4, "all"),
 )
+SPLIT_PAIRS = ("b1h1_l16k", "b1h2_l4k")
 
 
 def single_gpu_extras(torch, ops, dev, barrier, names=None):
@@ -307,7 +309,7 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
                    frac=round(f / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4))
         out[name] = rec
         del qq, kk, vv
-    for base in ("b2h2_l16k", "b1h2_l16k"):  # split against unsplit, same shape
+    for base in SPLIT_PAIRS:  # split against unsplit, same shape
         if f"{base}_splitkv" in out and f"{base}_unsplit" in out:
             out[f"{base}_splitkv"]["speedup_vs_unsplit"] = round(
                 out[f"{base}_unsplit"]["ms"] / out[f"{base}_splitkv"]["ms"], 3)

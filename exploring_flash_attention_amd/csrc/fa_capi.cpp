@@ -209,24 +209,26 @@ int device_cus() {
     return n;
 }
 
-// Workgroups of the split kernel (fused split mode, contiguous, with a key tail) the device
-// runs at once: the kernel's own launch bound (fa_internal.hpp kernel_wps) per CU.
-int resident_workgroups(int64_t d) {
-    return device_cus() * fa::kernel_wps((int)d, fa::kFused, true, false);
+// How many partial workgroups per query tile the split-KV schedule wants: none beyond the
+// first when the query tiles alone give every CU a workgroup, otherwise enough for one per CU.
+// (Measured, round 3: a single workgroup per CU -- one wave per SIMD -- already runs the d = 128
+// loop at 0.88x the throughput of two; splitting B1 H2 L16384 (256 query tiles) into 8 partials
+// per tile to reach two per CU lost 10 %, B2 H2 L16384 into 4 lost 13 %: every partial pays a
+// prologue, an epilogue and its round trip through the workspace.  Splits pay when CUs idle.)
+int64_t wanted_partials(int64_t items, int64_t cap) {
+    const int64_t ncu = device_cus();
+    int64_t ns = items >= ncu ? 1 : (ncu + items - 1) / items;
+    return ns < cap ? ns : cap;
 }
 
-// FA_KV_TILES_AUTO: pick the split from occupancy -- no split when the
-// query tiles alone fill the device twice over, else enough splits for about two
-// workgroups per slot (each split at least one KV tile).
+// FA_KV_TILES_AUTO: pick the split from occupancy: the KV tiles of a head
+// cut into wanted_partials() equal splits.
 int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
     if (BH <= 0 || L <= 0 || !supported_d(d)) return 1;  // the shape checks report these
     const int64_t bk = keys_per_tile(e, d);
     const int64_t ntiles = (L + bk - 1) / bk;
     const int64_t items = BH * ((L + rows_per_block(e) - 1) / rows_per_block(e));
-    const int64_t want = 2 * (int64_t)resident_workgroups(d);
-    if (items >= want) return (int)ntiles;
-    int64_t ns = (want + items - 1) / items;
-    if (ns > ntiles) ns = ntiles;
+    const int64_t ns = wanted_partials(items, ntiles);
     return (int)((ntiles + ns - 1) / ns);
 }
 
@@ -236,11 +238,11 @@ int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
 // query tile are grouped onto one workgroup: the blocks of a group are combined on chip (the
 // online softmax carried across them -- algebraically the reduction's formula, split after
 // split), the groups' partials through the workspace and the in-kernel reduction.  By default
-// (blocks_per_workgroup = FA_BLOCKS_PER_WG_AUTO) as many blocks go to one group as still leave
-// >= 4 workgroups per resident slot, so a problem whose query tiles already fill the GPU moves
-// no partials through HBM at all, and a short-batch long-sequence one gets one workgroup per
-// block; a positive blocks_per_workgroup fixes the group (1 = the reference's layout: one
-// workgroup and one HBM partial per block).  Planned once per call: the workspace size, the
+// (blocks_per_workgroup = FA_BLOCKS_PER_WG_AUTO) the blocks of a query tile are cut into
+// wanted_partials() equal groups: a problem whose query tiles already give every CU a
+// workgroup moves no partials through HBM at all, a short batch of long sequences gets just
+// enough partials to occupy every CU; a positive blocks_per_workgroup fixes the group (1 =
+// the reference's layout: one workgroup and one HBM partial per block).  Planned once per call: the workspace size, the
 // grid and the split length all come from the same SplitPlan.
 struct SplitPlan {
     int kvtpb;       // KV tiles per key block (FA_KV_TILES_AUTO resolved)
@@ -264,12 +266,8 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
     if (blocks_per_wg > 0) {
         p.group = blocks_per_wg < p.units ? blocks_per_wg : p.units;
     } else {
-        const int64_t want = 4 * (int64_t)resident_workgroups(d);
-        for (int g = p.units; g > 1; --g)
-            if (items * ((p.units + g - 1) / g) >= want) {
-                p.group = g;
-                break;
-            }
+        const int64_t ns = wanted_partials(items, p.units);
+        p.group = (int)((p.units + ns - 1) / ns);  // equal groups (the last one may be shorter)
     }
     p.launched = (p.units + p.group - 1) / p.group;
     const int64_t kw = keys * p.group;

@@ -23,6 +23,11 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
 
 template <typename T, typename PT, int MODE>
 static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
+#ifdef FA_LITE_D  // (scripts/build_lite.sh: one head dim, bf16 only, for fast A/B builds)
+    if constexpr (std::is_same_v<T, __bf16>)
+        return d == FA_LITE_D ? launch_one<T, PT, FA_LITE_D, MODE>(a, s) : hipErrorInvalidValue;
+    return hipErrorInvalidValue;
+#else
     switch (d) {
         case 32: return launch_one<T, PT, 32, MODE>(a, s);
         case 64: return launch_one<T, PT, 64, MODE>(a, s);
@@ -30,6 +35,7 @@ static hipError_t launch_d(int d, const FwdArgs& a, hipStream_t s) {
         case 256: return launch_one<T, PT, 256, MODE>(a, s);
         default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 hipError_t launch_fwd(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s) {

@@ -55,6 +55,9 @@ constexpr int kRowmaxFenceMask = 0x8;  // d = 256
 constexpr int kUniformWidMask = 0x1;   // d = 32
 constexpr int kNoTailMask = 0xD;       // d = 32, 128, 256
 constexpr int kPackedMaxD = 32;
+#ifndef FA_PIN
+#define FA_PIN 0  // (development: the pinned d = 128 step schedule)
+#endif
 // (the row-sum MFMA table, rs16_on, and the launch bounds, kernel_wps, live in
 // fa_internal.hpp: the host's split planner sizes its grids with the same occupancy)
 static_assert(fa::kernel_wps(32, 0, false, false) == 4 && fa::kernel_wps(64, 2, true, false) == 3 &&
@@ -473,6 +476,150 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
         __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
     };
 
+    // ---- the d = 128 steady step with a pinned instruction schedule (no key tail, 32-row
+    // waves).  The step is laid out as 36 MFMA slots, each closed by a scheduling barrier so
+    // that hipcc keeps every slot's fillers with its MFMA (it still allocates registers and
+    // inserts the hazard wait states):
+    //   phase A, 16 slots: QK^T(t+1), two accumulation chains (32-key blocks) alternating;
+    //     fillers: the FMA + exponential of 20 of tile t's 32 scores per lane, the packing of
+    //     the first key block's P fragments, the K reads KA slots ahead, the 8 DMA pieces;
+    //   phase B, 20 slots: P.V(t) by key block, (db, ss) inside, and the key block's two row-sum
+    //     MFMAs after it; fillers: the remaining 12 exponentials and the second key block's
+    //     packing (ahead of the MFMAs that read them), the V reads VA MFMAs ahead, the row max
+    //     of tile t+1 (its QK^T finished >= 8 slots earlier).
+    // Every LDS read is inline asm with an explicit counted lgkmcnt wait on the registers it
+    // fills (so neither hipcc's waitcnt pass nor the in-flight LDS-DMA is involved).
+    constexpr bool PIN = FA_PIN && D == 128 && RB == 1 && !TAIL;
+    constexpr int KA = 3, VA = 2;  // reads in flight: K fragments (slots), V operands (MFMAs)
+    const int swz = (l32 >> 2) & 3;
+    const unsigned kaddr_e = (unsigned)(size_t)kring + (l32 >> 3) * 2048 + 64 * (l32 & 7) + 16 * (hf ^ swz);
+    const unsigned kaddr_o = (unsigned)(size_t)kring + (l32 >> 3) * 2048 + 64 * (l32 & 7) + 16 * ((2 + hf) ^ swz);
+    auto step_pinned = [&](auto par_c, auto flags_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
+                           float (&mx)[RB]) {
+        constexpr int P = decltype(par_c)::value;
+        constexpr int F = decltype(flags_c)::value;
+        constexpr bool DMAK = F & 4;
+        static_assert(NKB == 2 && NKS == 8 && NDB == 4 && DPW == 4, "pinned schedule is for d = 128");
+        if (__builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr)) {
+            const float m_new = fmaxf(m[0], mx[0]);
+            const float alpha = __builtin_amdgcn_exp2f(m[0] - m_new);
+            m[0] = m_new;
+            ls16[0] *= __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_row, __builtin_bit_cast(int, alpha)));
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) o[0][db] *= alpha;
+        }
+        const float nm = -m[0];
+        // DMA descriptors of K(t+2) (zeros past the end) and V(t+1)
+        const __amdgpu_buffer_rsrc_t krs =
+            make_rsrc32((const char*)kbase + (int64_t)(t + 2) * TILEB, DMAK && t + 2 < ntiles ? TILEB : 0);
+        const __amdgpu_buffer_rsrc_t vrs = make_rsrc32((const char*)vbase + (int64_t)(t + 1) * TILEB, TILEB);
+        char* const kdst = kring + P * TILEB + wid * DPW * 1024;
+        char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
+
+        u32x4 kf[KA + 1];
+        // (inline asm in a nested generic lambda must not capture: every operand is a parameter)
+        auto kread_ = [](auto r_c, auto p_c, u32x4 (&kf)[KA + 1], unsigned ke, unsigned ko) {
+            constexpr int R = decltype(r_c)::value, KS = R / 2, B2 = R % 2, PP = decltype(p_c)::value;
+            constexpr int OFF = (1 - PP) * TILEB + B2 * 8192 + 512 * (KS >> 1);
+            if constexpr (KS & 1)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[R % (KA + 1)]) : "v"(ko), "i"(OFF) : "memory");
+            else
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[R % (KA + 1)]) : "v"(ke), "i"(OFF) : "memory");
+        };
+        auto kread = [&](auto r_c) { kread_(r_c, par_c, kf, kaddr_e, kaddr_o); };
+        auto lwait = [](auto n_c, u32x4& reg) {
+            asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(reg) : "i"(decltype(n_c)::value) : "memory");
+        };
+        auto lwait2 = [](auto n_c, u32x2 (&reg)[2]) {
+            asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(reg[0]), "+v"(reg[1]) : "i"(decltype(n_c)::value) : "memory");
+        };
+        auto ex = [&](auto e_c) {  // FMA + exponential of score e of tile t
+            constexpr int E = decltype(e_c)::value;
+            sc[0][E / 16][E % 16] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[0][E / 16][E % 16], c, nm));
+        };
+        u32x4 pbu[2][2];  // packed P^T fragments [b2][ss]
+        auto cvt = [&](auto k_c) {  // pair k of key block k / 8 -> fragment (k / 8, (k % 8) / 4), dword k % 4
+            constexpr int K = decltype(k_c)::value, B2 = K / 8, SS = (K % 8) / 4, J = K % 4;
+            pbu[B2][SS][J] = pack2<T>(sc[0][B2][8 * SS + 2 * J], sc[0][B2][8 * SS + 2 * J + 1]);
+        };
+        auto dma = [&](auto i_c) {
+            constexpr int I = decltype(i_c)::value;
+            if constexpr (I < 4) {
+                if constexpr (DMAK) dma16(krs, kdst + I * 1024, dma_src[I], 0);
+            } else {
+                dma16(vrs, vdst + (I - 4) * 1024, dma_src[I - 4], 0);
+            }
+        };
+
+        // ---- phase A: QK^T(t+1) || exp(t)
+#pragma unroll
+        for (int b2 = 0; b2 < NKB; ++b2) sn[0][b2] = f32x16{};
+        static_for<KA>([&](auto r_c) { kread(r_c); });
+        static_for<16>([&](auto s_c) {
+            constexpr int S = decltype(s_c)::value;
+            if constexpr (S + KA < 16) kread(std::integral_constant<int, S + KA>{});
+            constexpr int AFTER = (S + KA < 16 ? S + KA : 15) - S;  // K reads issued after read S
+            lwait(std::integral_constant<int, AFTER>{}, kf[S % (KA + 1)]);
+            sn[0][S % 2] = M::mma(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[0][S / 2], sn[0][S % 2]);
+            constexpr int E0 = S * 20 / 16, E1 = (S + 1) * 20 / 16;  // exponentials 0..19
+            static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
+            if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key block 0 packs
+            if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
+            __builtin_amdgcn_sched_barrier(0);
+        });
+
+        // ---- phase B: P.V(t) || exp(t) rest, row max(t+1)
+        // PV MFMA p (0..15): b2 = p / 8, db = (p % 8) / 2, ss = p % 2; its V^T operand is two
+        // transposed reads, issued VA MFMAs ahead
+        u32x2 vf[VA + 1][2];
+        auto vread_ = [](auto p_c, auto par, u32x2 (&vf)[VA + 1][2], unsigned vb0, unsigned vb1) {
+            constexpr int PP = decltype(p_c)::value, B2 = PP / 8, DB = (PP % 8) / 2, SS = PP % 2;
+            constexpr int OFF = decltype(par)::value * TILEB + 4 * B2 * 8 * ROWB + 512 * DB + SS * 2 * 8 * ROWB;
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][0]) : "v"(vb0), "i"(OFF) : "memory");
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][1]) : "v"(vb1), "i"(OFF + 8 * ROWB) : "memory");
+        };
+        auto vread = [&](auto p_c) { vread_(p_c, par_c, vf, vbase0, vbase1); };
+        float m4[4];
+        static_for<VA>([&](auto p_c) { vread(p_c); });
+        static_for<20>([&](auto j_c) {
+            constexpr int J = decltype(j_c)::value;
+            // slot J: PV MFMA p, or a row-sum MFMA (J = 8, 9: key block 0; 18, 19: key block 1)
+            constexpr bool RS = (J % 10) >= 8;
+            constexpr int PP = J < 10 ? J : J - 2;
+            if constexpr (!RS) {
+                if constexpr (PP + VA < 16) vread(std::integral_constant<int, PP + VA>{});
+                constexpr int AFTER = 2 * ((PP + VA < 16 ? PP + VA : 15) - PP);
+                lwait2(std::integral_constant<int, AFTER>{}, vf[PP % (VA + 1)]);
+                constexpr int B2 = PP / 8, DB = (PP % 8) / 2, SS = PP % 2;
+                const u32x4 vv = {vf[PP % (VA + 1)][0][0], vf[PP % (VA + 1)][0][1], vf[PP % (VA + 1)][1][0],
+                                  vf[PP % (VA + 1)][1][1]};
+                o[0][DB] = M::mma(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[B2][SS]), o[0][DB]);
+            } else {
+                constexpr int B2 = J / 10, SS = J % 2;
+                ls16[0] = M::mma16(sel16, __builtin_bit_cast(v8, pbu[B2][SS]), ls16[0]);
+            }
+            // exponentials 20..31 in slots 0..5, key block 1 packs in slots 2..9
+            if constexpr (J < 6) {
+                ex(std::integral_constant<int, 20 + 2 * J>{});
+                ex(std::integral_constant<int, 21 + 2 * J>{});
+            }
+            if constexpr (J >= 2 && J < 10) cvt(std::integral_constant<int, 8 + J - 2>{});
+            // row max of tile t+1 in slots 8..19: four chains of v_maximum3 over 8 scores each
+            if constexpr (J >= 8 && J < 16) {
+                constexpr int CH = (J - 8) / 2, H = (J - 8) % 2;  // chain, half
+                // chain CH holds scores i with i % 4 == CH of both key blocks
+                if constexpr (H == 0)
+                    m4[CH] = fmax_nc(fmax_nc(sn[0][0][CH], sn[0][0][CH + 4]), fmax_nc(sn[0][0][CH + 8], sn[0][0][CH + 12]));
+                else
+                    m4[CH] = fmax_nc(fmax_nc(m4[CH], fmax_nc(sn[0][1][CH], sn[0][1][CH + 4])),
+                                     fmax_nc(sn[0][1][CH + 8], sn[0][1][CH + 12]));
+            }
+            if constexpr (J == 17) mx[0] = pair_max(fmax_nc(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]))) * c;
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
+    };
+
     // prologue: K(0), V(0), K(1) -> LDS; S(0) = QK^T(0)
     dma_tile(kbase, kring, 0);
     dma_tile(vbase, vring, 0);
@@ -501,19 +648,25 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
         using NEXTLAST = std::integral_constant<int, 1 | 2>;   // t+1 is the last tile
         using NEXTLASTK = std::integral_constant<int, 1 | 2 | 4>;
         using LAST = std::integral_constant<int, 0>;
+        // (the pinned schedule for every step with a next tile; the last step has no QK^T)
+        auto run = [&](auto par_c, auto flags_c, int t, f32x16 (&sc)[RB][NKB], f32x16 (&sn)[RB][NKB],
+                       float (&mx)[RB]) {
+            if constexpr (PIN && (decltype(flags_c)::value & 1)) step_pinned(par_c, flags_c, t, sc, sn, mx);
+            else step(par_c, flags_c, t, sc, sn, mx);
+        };
         int t = 0;
         for (; t + 2 < ntiles; t += 2) {
             // step t: tile t+1 is never the last one here.  Step t+1 may prefetch K(t+3)
             // past the end: the buffer range check turns it into zeros nobody reads, which
             // keeps the step branch-free.
-            step(C0{}, STEADY{}, t, sa, sb, mx);
-            step(C1{}, NEXTLASTK{}, t + 1, sb, sa, mx);
+            run(C0{}, STEADY{}, t, sa, sb, mx);
+            run(C1{}, NEXTLASTK{}, t + 1, sb, sa, mx);
         }
         if (ntiles - t == 2) {  // t is even here
-            step(C0{}, NEXTLAST{}, t, sa, sb, mx);
-            step(C1{}, LAST{}, t + 1, sb, sa, mx);
+            run(C0{}, NEXTLAST{}, t, sa, sb, mx);
+            run(C1{}, LAST{}, t + 1, sb, sa, mx);
         } else {
-            step(C0{}, LAST{}, t, sa, sb, mx);
+            run(C0{}, LAST{}, t, sa, sb, mx);
         }
     }
 

@@ -1,0 +1,12 @@
+// Stubs of the launchers a "lite" A/B build leaves out (scripts/build_lite.sh): only the
+// contiguous bf16 forward of fa_fwd.hip is compiled there, so that one kernel variant builds
+// in seconds.  Never part of the product library.
+#include "../../exploring_flash_attention_amd/csrc/fa_internal.hpp"
+namespace fa {
+hipError_t launch_fwd_strided(Elem, Elem, int, Mode, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_combine(Elem, Elem, int, const CombineArgs&, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_fwd64(int, Mode, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_combine64(int, const CombineArgs&, hipStream_t) { return hipErrorInvalidValue; }
+int fwd64_rows_per_block() { return 64; }
+int fwd64_keys_per_tile() { return 16; }
+}  // namespace fa

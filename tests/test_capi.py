@@ -153,10 +153,19 @@ def test_workspace_size_and_v2_checks():
     # partial O + lse (fragment order, 128-row tiles: 4096 = 32 x 128) + one counter per tile
     assert nbytes.value == rows * 128 * 2 + rows * 4 + 32 * 8 * 32 * 4
     assert nbytes.value > 2 ** 32  # 64-bit sizes (the reference overflows int32 here)
-    # a short batch of long sequences: one workgroup per key block
+    # a short batch of long sequences: 64 query tiles, so 4 equal groups of the 32 key blocks
+    # give each of the 256 CUs a workgroup
     assert lib.fa_fwd_v2_split_plan(1, 1, 8192, 128, 4, AUTO, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
                                     ctypes.byref(p)) == 0
-    assert (kb.value, g.value, p.value) == (32, 1, 32)
+    assert (kb.value, g.value, p.value) == (32, 8, 4)
+    # 256 query tiles already occupy every CU: no split (measured: 8 partials there lose 10 %)
+    assert lib.fa_fwd_v2_split_plan(1, 2, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                    ctypes.byref(p)) == 0 and p.value == 1
+    # 128 query tiles: two partials each; 100 query tiles: 3 (groups of ceil(64/3) = 22 blocks)
+    assert lib.fa_fwd_v2_split_plan(1, 1, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                    ctypes.byref(p)) == 0 and (g.value, p.value) == (32, 2)
+    assert lib.fa_fwd_v2_split_plan(1, 1, 12800, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                    ctypes.byref(p)) == 0 and (g.value, p.value) == (17, 3)
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
                                         ctypes.byref(nbytes), ctypes.byref(ns)) == 0
     assert ns.value == 2
@@ -176,7 +185,7 @@ def test_workspace_size_and_v2_checks():
     assert ns.value == 1  # 8192 query tiles already fill the device
     assert lib.fa_fwd_v2_workspace_size(1, 1, 4096, 128, L.FA_KV_TILES_AUTO, L.FA_DTYPE_BF16,
                                         L.FA_DTYPE_FP32, ctypes.byref(nbytes), ctypes.byref(ns)) == 0
-    assert ns.value == 32  # 32 query tiles x 32 splits of 2 KV tiles ~ 2 per resident slot
+    assert ns.value == 8  # 32 query tiles x 8 splits of 8 KV tiles: one workgroup per CU
     fake = ctypes.c_void_p(0x10000)
     st = lib.fa_fwd_v2(fake, fake, fake, fake, 1, 1, 100, 64, 32, 32, 1, fake, 16, L.FA_DTYPE_FP16,
                        L.FA_DTYPE_FP32, NULL)
