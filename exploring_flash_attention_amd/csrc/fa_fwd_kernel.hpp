@@ -135,7 +135,11 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     const int lane = tid & 63;
     // wave-uniform and, where it pays, PROVABLY so (an SGPR): the LDS-DMA destinations (M0)
     // derived from it then need no v_readfirstlane per DMA
-    const int wid = (kUniformWidMask & d_bit(D)) ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+#ifndef FA_PIN_UWID
+#define FA_PIN_UWID 0
+#endif
+    const int wid = ((kUniformWidMask & d_bit(D)) || (FA_PIN_UWID && D == 128)) ? __builtin_amdgcn_readfirstlane(tid >> 6)
+                                                                               : tid >> 6;
     const int l32 = lane & 31;
     const int hf = lane >> 5;
 
@@ -490,7 +494,20 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     // Every LDS read is inline asm with an explicit counted lgkmcnt wait on the registers it
     // fills (so neither hipcc's waitcnt pass nor the in-flight LDS-DMA is involved).
     constexpr bool PIN = FA_PIN && D == 128 && RB == 1 && !TAIL;
-    constexpr int KA = 3, VA = 2;  // reads in flight: K fragments (slots), V operands (MFMAs)
+#ifndef FA_PIN_KA
+#define FA_PIN_KA 3
+#endif
+#ifndef FA_PIN_VA
+#define FA_PIN_VA 2
+#endif
+#ifndef FA_PIN_EXPA
+#define FA_PIN_EXPA 20
+#endif
+#ifndef FA_PIN_DMA
+#define FA_PIN_DMA 0
+#endif
+    constexpr int KA = FA_PIN_KA, VA = FA_PIN_VA;  // reads in flight: K fragments (slots), V operands (MFMAs)
+    constexpr int EXPA = FA_PIN_EXPA;  // exponentials in phase A (the rest: phase B, 2 per slot)
     const int swz = (l32 >> 2) & 3;
     const unsigned kaddr_e = (unsigned)(size_t)kring + (l32 >> 3) * 2048 + 64 * (l32 & 7) + 16 * (hf ^ swz);
     const unsigned kaddr_o = (unsigned)(size_t)kring + (l32 >> 3) * 2048 + 64 * (l32 & 7) + 16 * ((2 + hf) ^ swz);
@@ -561,10 +578,11 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             constexpr int AFTER = (S + KA < 16 ? S + KA : 15) - S;  // K reads issued after read S
             lwait(std::integral_constant<int, AFTER>{}, kf[S % (KA + 1)]);
             sn[0][S % 2] = M::mma(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[0][S / 2], sn[0][S % 2]);
-            constexpr int E0 = S * 20 / 16, E1 = (S + 1) * 20 / 16;  // exponentials 0..19
+            constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;  // exponentials 0..EXPA-1
             static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
             if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key block 0 packs
-            if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
+            if constexpr (FA_PIN_DMA == 0 && S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
+            if constexpr (FA_PIN_DMA == 2 && S % 4 == 1) dma(std::integral_constant<int, S / 4>{});
             __builtin_amdgcn_sched_barrier(0);
         });
 
@@ -598,12 +616,14 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
                 constexpr int B2 = J / 10, SS = J % 2;
                 ls16[0] = M::mma16(sel16, __builtin_bit_cast(v8, pbu[B2][SS]), ls16[0]);
             }
-            // exponentials 20..31 in slots 0..5, key block 1 packs in slots 2..9
-            if constexpr (J < 6) {
-                ex(std::integral_constant<int, 20 + 2 * J>{});
-                ex(std::integral_constant<int, 21 + 2 * J>{});
-            }
+            // exponentials EXPA..31 two per slot from slot 0, key block 1 packs in slots 2..9
+            // (EXPA in [20, 24]: every pack comes after its exponentials in program order)
+            static_assert(EXPA >= 20 && EXPA <= 24, "packs follow their exponentials in program order");
+            if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
+            if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
             if constexpr (J >= 2 && J < 10) cvt(std::integral_constant<int, 8 + J - 2>{});
+            if constexpr (FA_PIN_DMA == 1 && J < 8) dma(std::integral_constant<int, J>{});
+            if constexpr (FA_PIN_DMA == 2 && J % 4 == 1 && J < 17) dma(std::integral_constant<int, 4 + J / 4>{});
             // row max of tile t+1 in slots 8..19: four chains of v_maximum3 over 8 scores each
             if constexpr (J >= 8 && J < 16) {
                 constexpr int CH = (J - 8) / 2, H = (J - 8) % 2;  // chain, half

@@ -36,7 +36,91 @@ __global__ __launch_bounds__(256) void mfma_loop(float* sink, unsigned long long
     }
 }
 
-int main() {
+// The same loop on RANDOM operands: 8 A and 8 B fragments per lane (hash-generated bf16 in
+// [-2, 2)), a different (A, B) pair for every MFMA, as an attention or GEMM inner loop feeds
+// them.  Constant operands let the chip hold a higher clock (MI355X_MICROARCH.md, DVFS
+// give-back): this is the ceiling a random-data kernel can approach at the clock it holds.
+__device__ __forceinline__ unsigned hash32(unsigned x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+__global__ __launch_bounds__(256) void mfma_loop_rand(float* sink, unsigned long long* clk, int iters) {
+    bf16x8 a[8], b[8];
+    for (int f = 0; f < 8; ++f)
+        for (int j = 0; j < 8; ++j) {
+            const unsigned h = hash32(threadIdx.x * 977u + blockIdx.x * 7919u + f * 131u + j);
+            a[f][j] = (__bf16)((float)(h & 0xffff) / 16384.f - 2.f);
+            b[f][j] = (__bf16)((float)(h >> 16) / 16384.f - 2.f);
+        }
+    f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < iters; i += 2) {
+#pragma unroll
+        for (int f = 0; f < 8; f += 4) {
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f], b[f], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f + 1], b[f + 1], c1, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f + 2], b[f + 2], c2, 0, 0, 0);
+            c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[f + 3], b[f + 3], c3, 0, 0, 0);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    float s = 0.f;
+    for (int j = 0; j < 16; ++j) s += c0[j] + c1[j] + c2[j] + c3[j];
+    if (s == 12345.678f) sink[threadIdx.x] = s;
+    if (threadIdx.x == 0) {
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+template <typename K>
+static int run(K kernel, const char* label, int ncu, int khz) {
+    const int blocks = ncu * 2;  // 2 x 4 waves per CU = 2 waves per SIMD
+    const int iters = 20000;
+    float* sink;
+    unsigned long long* clk;
+    (void)hipMalloc(&sink, 256 * sizeof(float));
+    (void)hipMalloc(&clk, 2 * blocks * sizeof(unsigned long long));
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int w = 0; w < 20; ++w) kernel<<<blocks, 256>>>(sink, clk, iters);  // clock ramp
+    (void)hipEventRecord(e0);
+    const int reps = 20;
+    for (int r = 0; r < reps; ++r) kernel<<<blocks, 256>>>(sink, clk, iters);
+    (void)hipEventRecord(e1);
+    if (hipEventSynchronize(e1) != hipSuccess) return 1;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long* h = new unsigned long long[2 * blocks];
+    (void)hipMemcpy(h, clk, 2 * blocks * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    double mhz_sum = 0.0;
+    for (int i = 0; i < blocks; ++i) mhz_sum += (double)h[2 * i] / ((double)h[2 * i + 1] / 100.0);
+    const double mhz = mhz_sum / blocks;  // s_memrealtime ticks at 100 MHz
+    const double flops = 2.0 * 32 * 32 * 16 * 4.0 * iters * (blocks * 4.0) * reps;
+    const double tflops = flops / (ms * 1e-3) / 1e12;
+    printf("{\"operands\": \"%s\", \"cus\": %d, \"rated_clock_mhz\": %.0f, \"held_clock_mhz\": %.0f, "
+           "\"mfma_bf16_tflops\": %.1f, \"peak_at_rated_clock_tflops\": %.1f, \"peak_at_held_clock_tflops\": %.1f, "
+           "\"kernel\": \"4 independent v_mfma_f32_32x32x16_bf16 chains per wave, 2 waves per SIMD\"}\n",
+           label, ncu, khz / 1000.0, mhz, tflops, 4096.0 * ncu * khz * 1e3 / 1e12, 4096.0 * ncu * mhz * 1e6 / 1e12);
+    delete[] h;
+    return 0;
+}
+
+int main_rand_and_const() {
+    int dev = 0, ncu = 0, khz = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, dev);
+    if (run(mfma_loop, "constant", ncu, khz)) return 1;
+    return run(mfma_loop_rand, "random", ncu, khz);
+}
+
+int main() { return main_rand_and_const(); }
+
+int main_constant_only() {
     int dev = 0, ncu = 0, khz = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (one counter group per pass, --kernel-trace only, never with sys/runtime trace)
 # over scripts/run_kernel.py.  Usage: bash scripts/profile_pmc.sh [config] [name] ; output
-# gpurun_out/pmc_<name>/ (name defaults to the config; environment, e.g. FA_SPLIT_GROUP, passes through)
+# gpurun_out/pmc_<name>/ (name defaults to the config)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 CFG=${1:-c3}

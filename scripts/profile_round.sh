@@ -16,9 +16,12 @@ for cfg in c3 c2 c4; do
   bash scripts/profile_pmc.sh $cfg || exit $?
   python scripts/traffic.py gpurun_out/pmc_$cfg $cfg $OUT/hbm_traffic.json > /dev/null || exit $?
 done
-# C4 with 4 key blocks per workgroup (4 partials per query tile through the workspace)
-FA_SPLIT_GROUP=4 bash scripts/profile_pmc.sh c4 c4g4 || exit $?
-python scripts/traffic.py gpurun_out/pmc_c4g4 c4g4 $OUT/hbm_traffic.json > /dev/null || exit $?
+# C4 with 4 key blocks per workgroup (4 partials per query tile through the workspace), and a
+# shape the library splits itself (B1 H1 L16384: 2 partials per query tile)
+for cfg in c4g4 b1h1l16k; do
+  bash scripts/profile_pmc.sh $cfg || exit $?
+  python scripts/traffic.py gpurun_out/pmc_$cfg $cfg $OUT/hbm_traffic.json > /dev/null || exit $?
+done
 cat $OUT/kernel_stats.csv | head -3
 python - <<'PY'
 import json

@@ -1,6 +1,11 @@
 """Launch one forward configuration a few times (for rocprofv3 runs).
 
-    python scripts/run_kernel.py [c2|c3|c4|c5] [iters]
+    python scripts/run_kernel.py [config] [iters]
+
+configs: c2, c3 (FA-v1), c4 (split-KV, KV_TILES_PER_BLOCK = 4, the library's grouping), c4g4 /
+c4g1 (C4 with 4 / 1 key blocks per workgroup: 4 / 16 partials per query tile), b1h1l16k (a
+shape the library splits itself: 2 partials per query tile), b1h1l16k_unsplit (the same shape,
+one workgroup per query tile), c5 (one rank's C5 partial kernel shape, FA-v1 form).
 """
 import os
 import sys
@@ -10,17 +15,24 @@ import torch  # noqa: E402
 
 from exploring_flash_attention_amd import ops  # noqa: E402
 
-CFG = {"c2": (32, 8, 1024, 32, "v1"), "c3": (32, 8, 1024, 128, "v1"),
-       "c4": (32, 8, 4096, 128, "v2"), "c5": (32, 8, 16384, 128, "v1")}
+CFG = {"c2": (32, 8, 1024, 32, "v1", None), "c3": (32, 8, 1024, 128, "v1", None),
+       "c4": (32, 8, 4096, 128, "v2", None), "c4g4": (32, 8, 4096, 128, "v2", 4),
+       "c4g1": (32, 8, 4096, 128, "v2", 1), "b1h1l16k": (1, 1, 16384, 128, "v2", None),
+       "b1h1l16k_unsplit": (1, 1, 16384, 128, "v2", 64), "c5": (32, 8, 16384, 128, "v1", None)}
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-B, H, L, d, var = CFG[name]
+B, H, L, d, var, grp = CFG[name]
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn(B, H, L, d, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+out = torch.empty_like(q)
+ws = None
+if var == "v2":
+    nb, _ = ops.v2_workspace_bytes(B, H, L, d, 4, q.dtype, blocks_per_workgroup=grp)
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
 for _ in range(iters):
     if var == "v1":
-        ops.attention_v1(q, k, v)
+        ops.attention_v1(q, k, v, out=out)
     else:
-        ops.attention_v2(q, k, v, 4)
+        ops.attention_v2(q, k, v, 4, out=out, workspace=ws, blocks_per_workgroup=grp)
 torch.cuda.synchronize()
 print("done", name, iters)
