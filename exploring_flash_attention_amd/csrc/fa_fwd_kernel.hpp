@@ -55,9 +55,6 @@ constexpr int kRowmaxFenceMask = 0x8;  // d = 256
 constexpr int kUniformWidMask = 0x1;   // d = 32
 constexpr int kNoTailMask = 0xD;       // d = 32, 128, 256
 constexpr int kPackedMaxD = 32;
-#ifndef FA_PIN
-#define FA_PIN 0  // (development: the pinned d = 128 step schedule)
-#endif
 // (the row-sum MFMA table, rs16_on, and the launch bounds, kernel_wps, live in
 // fa_internal.hpp: the host's split planner sizes its grids with the same occupancy)
 static_assert(fa::kernel_wps(32, 0, false, false) == 4 && fa::kernel_wps(64, 2, true, false) == 3 &&
@@ -135,11 +132,9 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     const int lane = tid & 63;
     // wave-uniform and, where it pays, PROVABLY so (an SGPR): the LDS-DMA destinations (M0)
     // derived from it then need no v_readfirstlane per DMA
-#ifndef FA_PIN_UWID
-#define FA_PIN_UWID 0
-#endif
-    const int wid = ((kUniformWidMask & d_bit(D)) || (FA_PIN_UWID && D == 128)) ? __builtin_amdgcn_readfirstlane(tid >> 6)
-                                                                               : tid >> 6;
+    // (the pinned d = 128 step, below, measured +0.5 % with it; the compiler-scheduled one -2.5 %)
+    constexpr bool PIN = D == 128 && RB == 1 && !TAIL;
+    const int wid = ((kUniformWidMask & d_bit(D)) || PIN) ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int l32 = lane & 31;
     const int hf = lane >> 5;
 
@@ -493,21 +488,12 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     //     of tile t+1 (its QK^T finished >= 8 slots earlier).
     // Every LDS read is inline asm with an explicit counted lgkmcnt wait on the registers it
     // fills (so neither hipcc's waitcnt pass nor the in-flight LDS-DMA is involved).
-    constexpr bool PIN = FA_PIN && D == 128 && RB == 1 && !TAIL;
-#ifndef FA_PIN_KA
-#define FA_PIN_KA 3
-#endif
-#ifndef FA_PIN_VA
-#define FA_PIN_VA 2
-#endif
-#ifndef FA_PIN_EXPA
-#define FA_PIN_EXPA 20
-#endif
-#ifndef FA_PIN_DMA
-#define FA_PIN_DMA 0
-#endif
-    constexpr int KA = FA_PIN_KA, VA = FA_PIN_VA;  // reads in flight: K fragments (slots), V operands (MFMAs)
-    constexpr int EXPA = FA_PIN_EXPA;  // exponentials in phase A (the rest: phase B, 2 per slot)
+    // Measured (round 3, A/B in one process): 2.74k -> 2.56k cycles per step at C3, C3 +3.1 %,
+    // C4 +3.2 % wall (the chip holds a lower clock as the MFMAs pack closer: the loop is power-
+    // bound); K / V reads one slot deeper, 24 exponentials in phase A: same;
+    // the DMA pieces in phase B: C4 -3 %.
+    constexpr int KA = 3, VA = 2;  // reads in flight: K fragments (slots), V operands (MFMAs)
+    constexpr int EXPA = 20;       // exponentials in phase A (the rest: phase B, 2 per slot)
     const int swz = (l32 >> 2) & 3;
     const unsigned kaddr_e = (unsigned)(size_t)kring + (l32 >> 3) * 2048 + 64 * (l32 & 7) + 16 * (hf ^ swz);
     const unsigned kaddr_o = (unsigned)(size_t)kring + (l32 >> 3) * 2048 + 64 * (l32 & 7) + 16 * ((2 + hf) ^ swz);
@@ -526,10 +512,13 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             for (int db = 0; db < NDB; ++db) o[0][db] *= alpha;
         }
         const float nm = -m[0];
-        // DMA descriptors of K(t+2) (zeros past the end) and V(t+1)
+        // DMA descriptors of K(t+2) (zeros past the end) and V(t+1), as dma_tile makes them
+        constexpr int64_t TSTRIDE = STRIDED ? 0 : TILEB;  // (strided: kBK rows of krb bytes)
+        const int64_t tstride = STRIDED ? (int64_t)kBK * krb : TSTRIDE;
+        const int tbytes = STRIDED ? (kBK - 1) * krb + ROWB : TILEB;
         const __amdgpu_buffer_rsrc_t krs =
-            make_rsrc32((const char*)kbase + (int64_t)(t + 2) * TILEB, DMAK && t + 2 < ntiles ? TILEB : 0);
-        const __amdgpu_buffer_rsrc_t vrs = make_rsrc32((const char*)vbase + (int64_t)(t + 1) * TILEB, TILEB);
+            make_rsrc32((const char*)kbase + (int64_t)(t + 2) * tstride, DMAK && t + 2 < ntiles ? tbytes : 0);
+        const __amdgpu_buffer_rsrc_t vrs = make_rsrc32((const char*)vbase + (int64_t)(t + 1) * tstride, tbytes);
         char* const kdst = kring + P * TILEB + wid * DPW * 1024;
         char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
 
@@ -581,8 +570,7 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;  // exponentials 0..EXPA-1
             static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
             if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key block 0 packs
-            if constexpr (FA_PIN_DMA == 0 && S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
-            if constexpr (FA_PIN_DMA == 2 && S % 4 == 1) dma(std::integral_constant<int, S / 4>{});
+            if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
             __builtin_amdgcn_sched_barrier(0);
         });
 
@@ -622,8 +610,6 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
             if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
             if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
             if constexpr (J >= 2 && J < 10) cvt(std::integral_constant<int, 8 + J - 2>{});
-            if constexpr (FA_PIN_DMA == 1 && J < 8) dma(std::integral_constant<int, J>{});
-            if constexpr (FA_PIN_DMA == 2 && J % 4 == 1 && J < 17) dma(std::integral_constant<int, 4 + J / 4>{});
             // row max of tile t+1 in slots 8..19: four chains of v_maximum3 over 8 scores each
             if constexpr (J >= 8 && J < 16) {
                 constexpr int CH = (J - 8) / 2, H = (J - 8) % 2;  // chain, half
