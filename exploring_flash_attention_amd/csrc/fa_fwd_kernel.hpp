@@ -491,7 +491,8 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     // Measured (round 3, A/B in one process): 2.74k -> 2.56k cycles per step at C3, C3 +3.1 %,
     // C4 +3.2 % wall (the chip holds a lower clock as the MFMAs pack closer: the loop is power-
     // bound); K / V reads one slot deeper, 24 exponentials in phase A: same;
-    // the DMA pieces in phase B: C4 -3 %.
+    // the DMA pieces in phase B: C4 -3 %; VALU row sums instead of the row-sum MFMAs: C3 -1.5 %,
+    // C4 -2.5 %; s_setprio by step parity (three patterns): C3 0, C4 -1.5 ... -2.3 %.
     constexpr int KA = 3, VA = 2;  // reads in flight: K fragments (slots), V operands (MFMAs)
     constexpr int EXPA = 20;       // exponentials in phase A (the rest: phase B, 2 per slot)
     const int swz = (l32 >> 2) & 3;

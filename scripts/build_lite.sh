@@ -10,14 +10,14 @@ CS=exploring_flash_attention_amd/csrc
 OUT=exploring_flash_attention_amd/_lib/ab
 mkdir -p $OUT /tmp/fa_lite
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=fast -fno-slp-vectorize -mllvm --amdgpu-mfma-vgpr-form"
-/opt/rocm/bin/hipcc $FL -x hip -c $CS/fa_capi.cpp -o /tmp/fa_lite/capi.o
 /opt/rocm/bin/hipcc $FL -x hip -c scripts/lite/fa_lite_stubs.cpp -o /tmp/fa_lite/stubs.o
 pids=()
 names=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   ( /opt/rocm/bin/hipcc $FL -DFA_LITE_D=$D $flags -x hip -c $CS/fa_fwd.hip -o /tmp/fa_lite/$name.o &&
-    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/$name.so /tmp/fa_lite/$name.o /tmp/fa_lite/capi.o /tmp/fa_lite/stubs.o &&
+    /opt/rocm/bin/hipcc $FL $flags -x hip -c $CS/fa_capi.cpp -o /tmp/fa_lite/$name.capi.o &&
+    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/$name.so /tmp/fa_lite/$name.o /tmp/fa_lite/$name.capi.o /tmp/fa_lite/stubs.o &&
     echo "built $name ($flags)" ) &
   pids+=($!)
 done
