@@ -228,8 +228,11 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     // A of the RS16 MFMA: output rows 0-7 sum lane groups 0 and 2 (query n, both key halves),
     // rows 8-15 groups 1 and 3 (query n + 16)
     v8 sel16;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sel16[j] = static_cast<T>(((lane & 15) < 8) == (((lane >> 4) & 1) == 0) ? 1.f : 0.f);
+    {
+        constexpr unsigned kOne = std::is_same_v<T, __bf16> ? 0x3F80u : 0x3C00u;  // 1.0 in T
+        const unsigned e = ((lane & 15) < 8) == (((lane >> 4) & 1) == 0) ? kOne | (kOne << 16) : 0u;
+        sel16 = __builtin_bit_cast(v8, u32x4{e, e, e, e});
+    }
     const int rs16_src = ((lane & 31) < 16 ? (lane & 31) : (lane & 31) + 16) * 4;  // holder of own row
     const int rs16_row = ((lane & 15) + 16 * (lane >> 5)) * 4;                      // row held here
 #pragma unroll
@@ -644,6 +647,10 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     qk(kring, sa);
     if constexpr (TAIL) mask(0, sa);
     rowmax(sa, mx);
+    // the reference max starts at tile 0's row max (every tile holds a valid key): step 0
+    // then never takes the rescale branch that a -inf start would force on every workgroup
+#pragma unroll
+    for (int r = 0; r < RB; ++r) m[r] = mx[r];
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
     FA_STAMP(2);
 
