@@ -75,6 +75,42 @@ __global__ __launch_bounds__(256) void mfma_loop_rand(float* sink, unsigned long
     }
 }
 
+// Operand patterns on the same random fragments (which operand changes from one MFMA to the
+// next): MFMA k of a group of 8 reads A fragment ia(k) and B fragment ib(k).
+//   0 both change every MFMA (= mfma_loop_rand)       1 A repeats in pairs (k, k+1), B changes
+//   2 B repeats in pairs, A changes (the QK^T order)  3 A constant, B changes
+//   4 B constant, A changes                           5 both constant (random values)
+template <int MODE>
+__global__ __launch_bounds__(256) void mfma_loop_pattern(float* sink, unsigned long long* clk, int iters) {
+    bf16x8 a[8], b[8];
+    for (int f = 0; f < 8; ++f)
+        for (int j = 0; j < 8; ++j) {
+            const unsigned h = hash32(threadIdx.x * 977u + blockIdx.x * 7919u + f * 131u + j);
+            a[f][j] = (__bf16)((float)(h & 0xffff) / 16384.f - 2.f);
+            b[f][j] = (__bf16)((float)(h >> 16) / 16384.f - 2.f);
+        }
+    f32x16 c[4] = {};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < iters; i += 2) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int ia = MODE == 1 ? (k & ~1) : MODE == 3 || MODE == 5 ? 0 : k;
+            const int ib = MODE == 2 ? (k & ~1) : MODE == 4 || MODE == 5 ? 0 : k;
+            c[k & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ia], b[ib], c[k & 3], 0, 0, 0);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    float s = 0.f;
+    for (int j = 0; j < 16; ++j) s += c[0][j] + c[1][j] + c[2][j] + c[3][j];
+    if (s == 12345.678f) sink[threadIdx.x] = s;
+    if (threadIdx.x == 0) {
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
 template <typename K>
 static int run(K kernel, const char* label, int ncu, int khz) {
     const int blocks = ncu * 2;  // 2 x 4 waves per CU = 2 waves per SIMD
@@ -115,7 +151,12 @@ int main_rand_and_const() {
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, dev);
     if (run(mfma_loop, "constant", ncu, khz)) return 1;
-    return run(mfma_loop_rand, "random", ncu, khz);
+    if (run(mfma_loop_rand, "random", ncu, khz)) return 1;
+    if (run(mfma_loop_pattern<1>, "random, A repeated in pairs", ncu, khz)) return 1;
+    if (run(mfma_loop_pattern<2>, "random, B repeated in pairs", ncu, khz)) return 1;
+    if (run(mfma_loop_pattern<3>, "random, A constant", ncu, khz)) return 1;
+    if (run(mfma_loop_pattern<4>, "random, B constant", ncu, khz)) return 1;
+    return run(mfma_loop_pattern<5>, "random values, both constant", ncu, khz);
 }
 
 int main() { return main_rand_and_const(); }

@@ -177,6 +177,23 @@ def test_matrix(gpu, variant, dtype, d):
         _gate(out, _ref(q, k, v), dtype)
 
 
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+def test_tile_counts_without_tail(gpu, d):
+    """1 ... 7 whole 64-key tiles: every entry into the unrolled two-step loop (no steady
+    pair, one pair, a pair and an odd last step) of the no-tail kernels -- at d = 128 the
+    pinned step -- fused, and split-KV with key blocks of 1 and 4 tiles."""
+    from exploring_flash_attention_amd import ops
+    for n in range(1, 8):
+        L = 64 * n
+        q, k, v = _inputs(1, 2, L, d, torch.bfloat16, seed=40 + n)
+        ref = _ref(q, k, v)
+        for fn in (ops.attention_v1, lambda a, b, c: ops.attention_v2(a, b, c, 1),
+                   lambda a, b, c: ops.attention_v2(a, b, c, 4)):
+            out = fn(q.to(gpu), k.to(gpu), v.to(gpu))
+            torch.cuda.synchronize()
+            _gate(out, ref, torch.bfloat16)
+
+
 @pytest.mark.parametrize("d", [8, 16, 48, 80, 96, 160, 200])
 def test_head_dims_without_a_kernel(gpu, d):
     """Any 1 <= d <= 256: zero-padded to the next kernel head dim with the scale 1/sqrt(d)
