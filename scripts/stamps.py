@@ -101,6 +101,28 @@ def main():
             prev = [b_ for b_ in ends if b_ <= a_]
             if prev:
                 gaps.append(a_ - prev[-1])
+    # how the CU's resident workgroups' KV loops overlap: each workgroup's loop interval mapped
+    # onto the realtime clock (its own memtime -> realtime line), then per CU the time with 0, 1
+    # and 2 workgroups inside their loops, from the CU's first entry to its last end
+    scale = (end - ent) / np.maximum(s[:, 5] - s[:, 0], 1)
+    lo_a = ent + (s[:, 2] - s[:, 0]) * scale
+    lo_b = ent + (s[:, 3] - s[:, 0]) * scale
+    cu_loops = collections.defaultdict(list)
+    for w in range(nwg):
+        cu_loops[(int(s[w, 7]) & 0xF, (int(s[w, 6]) >> 8) & 0xFF)].append((lo_a[w], lo_b[w], ent[w], end[w]))
+    in_loop = np.zeros(3)
+    for wgs in cu_loops.values():
+        ev = sorted([(a_, 1) for a_, _, _, _ in wgs] + [(b_, -1) for _, b_, _, _ in wgs])
+        t0, t1 = min(x[2] for x in wgs), max(x[3] for x in wgs)
+        occ, last = 0, t0
+        for t, dlt in ev:
+            in_loop[min(occ, 2)] += t - last
+            occ += dlt
+            last = t
+        in_loop[0] += t1 - last
+    in_loop /= in_loop.sum()
+    print(f"  CU time with 0 / 1 / 2 workgroups inside their KV loops: "
+          f"{in_loop[0]:.1%} / {in_loop[1]:.1%} / {in_loop[2]:.1%}")
     total = end.max()
     print(f"  slot-time lost with < 2 resident workgroups (until the kernel's last end): "
           f"{np.mean([u + (total - le) for u, le in zip(under, last_end)]) / total:.1%} of 2 x span per CU"
