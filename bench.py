@@ -493,7 +493,8 @@ def main():
         if cfg["variant"] == "v1":
             def step():
                 ops.attention_v1(q, k, v, out=out)
-            kernel = "fa_fwd_kernel (final)"
+            kernel = ("fa_fwd16_kernel (final, 16x16x32 MFMA)" if d == 128 and L % 64 == 0
+                      else "fa_fwd_kernel (final)")
         else:
             nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -502,7 +503,7 @@ def main():
                 ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
             _, _, ppt = ops.v2_split_plan(B, H, L, d, cfg["kvtpb"], q.dtype)
             kernel = ("fa_fwd_kernel (split-KV, in-kernel combine)" if ppt > 1
-                      else "fa_fwd_kernel (final: the library groups every key block of a query tile "
+                      else "fa_fwd16_kernel (final: the library groups every key block of a query tile "
                            "on one workgroup, fa_fwd_v2_split_plan)")
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         work = flops(B, H, L, d)

@@ -3,6 +3,11 @@
 // unit, so the two instantiation sets compile in parallel).
 #define FA_FWD_MAIN_TU
 #include "fa_fwd_kernel.hpp"
+#include "fa_fwd16_kernel.hpp"
+
+#ifndef FA_SHAPE16
+#define FA_SHAPE16 1
+#endif
 
 namespace fa {
 
@@ -12,6 +17,12 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
+    if constexpr (FA_SHAPE16 && D == 128 && MODE == kFinal) {
+        if (a.Lk % bk_for(D) == 0) {  // no key tail (final mode: one split)
+            hipLaunchKernelGGL((fa_fwd16_kernel<T, D>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
+            return hipGetLastError();
+        }
+    }
     if (a.Lk % bk_for(D) || !(kNoTailMask & d_bit(D)))
         hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads),
                            lds, s, a);

@@ -21,7 +21,7 @@ out = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
-        if "fa_fwd_kernel" in row.get("Kernel_Name", ""):
+        if "fa_fwd_kernel" in row.get("Kernel_Name", "") or "fa_fwd16_kernel" in row.get("Kernel_Name", ""):
             acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k in sorted(acc):
     v = acc[k]

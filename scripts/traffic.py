@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -21,7 +22,7 @@ def main():
     vals = {}
     for f in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "fa_fwd_kernel" not in r["Kernel_Name"]:
+            if not re.search(r"fa_fwd(16)?_kernel", r["Kernel_Name"]):
                 continue
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     mean = {k: sum(v) / len(v) for k, v in vals.items()}
