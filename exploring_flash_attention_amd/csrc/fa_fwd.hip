@@ -17,9 +17,9 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
-    if constexpr (FA_SHAPE16 && D == 128 && MODE == kFinal) {
-        if (a.Lk % bk_for(D) == 0) {  // no key tail (final mode: one split)
-            hipLaunchKernelGGL((fa_fwd16_kernel<T, D>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
+    if constexpr (FA_SHAPE16 && D == 128) {
+        if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {  // no key tail in any split
+            hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();
         }
     }

@@ -49,6 +49,8 @@ __device__ __forceinline__ void quad_max2(float x0, float x1, float& m0, float& 
     m1 = __uint_as_float(u[1]);
 }
 
+template <typename X> struct TypeTag { using type = X; };
+
 #ifndef FA16_PIN
 #define FA16_PIN 1
 #endif
@@ -62,7 +64,10 @@ __device__ __forceinline__ void quad_max2(float x0, float x1, float& m0, float& 
 #define FA16_EXPA 28
 #endif
 
-template <typename T, int D>
+// MODE: kFinal (O), kPartial (normalised partial O + lse in row layout, fa_combine.hip reads
+// them) or kFused (partials in fragment order, combined by the last workgroup of each query
+// tile), as fa_fwd_kernel.hpp; every split a multiple of 64 keys and non-empty.
+template <typename T, typename PT, int D, int MODE>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
@@ -86,19 +91,23 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
 
     const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int qt = w % a.nqt;
-    const int64_t bh = w / a.nqt;  // final mode: one split
+    const int rest = w / a.nqt;
+    const int split = rest % a.nsplit;
+    const int64_t bh = rest / a.nsplit;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n16 = lane & 15, g = lane >> 4;
-    const int ntiles = (int)(a.Lk / kBK);
+    const int64_t kv_begin = (int64_t)split * a.kv_per_split;
+    const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
+    const int ntiles = (int)((kv_end - kv_begin) / kBK);
 
     const int64_t q_tile0 = (int64_t)qt * kBQ;
     const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D + q_tile0 * D;
     const int64_t q_rows = a.Lq - q_tile0 < kBQ ? a.Lq - q_tile0 : kBQ;
     const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, q_rows * ROWB);
-    const unsigned short* const kbase = (const unsigned short*)a.k + bh * a.Lk * D;
-    const unsigned short* const vbase = (const unsigned short*)a.v + bh * a.Lk * D;
+    const unsigned short* const kbase = (const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D;
+    const unsigned short* const vbase = (const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D;
 
     // The 32 dims of a QK^T k-step are split over the lane groups g as 8-dim chunk pg(g) =
     // (0, 3, 1, 2)[g] (A and B agree, so the sum is the same): ds_read_b128 serves a wave in the
@@ -381,25 +390,188 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         }
     }
 
-    // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n]; dv blocks 2e and
-    // 2e+1 are paired by one v_permlane16_swap per dword so that each lane stores 16 bytes:
-    // lane group g stores columns 32*e + 16*(g&1) + 8*(g>>1) .. +7
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb) {
-        const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
-        const float inv = 1.f / rs[qb][0];
-        if (q_row >= a.Lq) continue;
-        unsigned short* const Oh = (unsigned short*)a.o + bh * a.Lq * D + q_row * D;
+    // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n].  A 16-bit row is
+    // stored 16 bytes per lane: dv blocks 2e and 2e+1 are paired by one v_permlane16_swap per
+    // dword, lane group g then holds columns 32*e + 16*(g&1) + 8*(g>>1) .. +7.
+    auto store_row16 = [&](auto ph_c, unsigned short* Oh, const f32x4 (&v)[NDB], float scale) {
+        using PH = typename decltype(ph_c)::type;
 #pragma unroll
         for (int e = 0; e < NDB / 2; ++e) {
-            const unsigned x0 = pack2<T>(o[2 * e][qb][0] * inv, o[2 * e][qb][1] * inv);
-            const unsigned x1 = pack2<T>(o[2 * e][qb][2] * inv, o[2 * e][qb][3] * inv);
-            const unsigned y0 = pack2<T>(o[2 * e + 1][qb][0] * inv, o[2 * e + 1][qb][1] * inv);
-            const unsigned y1 = pack2<T>(o[2 * e + 1][qb][2] * inv, o[2 * e + 1][qb][3] * inv);
+            const unsigned x0 = pack2<PH>(v[2 * e][0] * scale, v[2 * e][1] * scale);
+            const unsigned x1 = pack2<PH>(v[2 * e][2] * scale, v[2 * e][3] * scale);
+            const unsigned y0 = pack2<PH>(v[2 * e + 1][0] * scale, v[2 * e + 1][1] * scale);
+            const unsigned y1 = pack2<PH>(v[2 * e + 1][2] * scale, v[2 * e + 1][3] * scale);
             const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
             const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
             const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
             *(u32x4*)(Oh + 32 * e + 16 * (g & 1) + 8 * (g >> 1)) = u;
+        }
+    };
+    f32x4 ov[NQB][NDB];  // O by query block
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) ov[qb][db] = o[db][qb];
+    float lsum[NQB], inv[NQB];
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) {
+        lsum[qb] = rs[qb][0];
+        inv[qb] = 1.f / lsum[qb];
+    }
+    constexpr bool SCALED = std::is_same_v<PT, f16s_t>;   // fp16 partials, per-row 2^-e
+    using PH = std::conditional_t<SCALED, _Float16, T>;   // 16-bit partial element type
+    float esc[NQB] = {0.f, 0.f};
+    if constexpr (MODE != kFinal && SCALED) {
+        // the row's largest |O / l| just below 1 after the exact scale 2^-e
+        float mxa[NQB];
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            float mx = 0.f;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mx = fmax_nc(mx, __builtin_fabsf(ov[qb][db][i]));
+            mxa[qb] = mx;
+        }
+        quad_max2(mxa[0], mxa[1], mxa[0], mxa[1]);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            const int e = __builtin_amdgcn_frexp_expf(mxa[qb] * inv[qb]);
+            esc[qb] = (float)e;
+            inv[qb] = __builtin_amdgcn_ldexpf(inv[qb], -e);
+        }
+    }
+    if constexpr (MODE == kFinal) {
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
+            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o + (bh * a.Lq + q_row) * D, ov[qb], inv[qb]);
+        }
+    } else if constexpr (MODE == kPartial) {
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
+            if (q_row >= a.Lq) continue;
+            const int64_t chunk = q_row / a.chunk_rows, r_in = q_row % a.chunk_rows;
+            const int64_t row_lin = chunk * a.BH * a.chunk_rows + bh * a.chunk_rows + r_in;
+            PT* const Op = (PT*)a.o + split * a.split_stride + row_lin * D;
+            if constexpr (sizeof(PT) == 4) {
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) *(f32x4*)((float*)Op + 16 * db + 4 * g) = ov[qb][db] * inv[qb];
+            } else {
+                store_row16(TypeTag<PH>{}, (unsigned short*)Op, ov[qb], inv[qb]);
+            }
+            // lse in log2 units: m + log2(l)  (v_log_f32 is log2)
+            const float lse = m[qb] + __builtin_amdgcn_logf(lsum[qb]);
+            if (g == 0) {
+                if constexpr (SCALED)
+                    *(float2*)(a.lse + 2 * (split * a.BH * a.Lq + row_lin)) = make_float2(lse, esc[qb]);
+                else
+                    a.lse[split * a.BH * a.Lq + row_lin] = lse;
+            }
+        }
+    } else {
+        // Split-KV partials combined on chip (fa_fwd_kernel.hpp's protocol and workspace
+        // layout): every workgroup stores its normalised partial O (PT) and lse in FRAGMENT
+        // order -- lane-linear pieces, coalesced for the stores and the combine's loads; the
+        // workgroup that arrives last at its query tile's counter (stores sc1, vmcnt(0), a
+        // barrier, one agent-scope atomic) reads the other splits' partials and writes O.
+        constexpr int SC1 = 16;                // cache-policy bit: sc1
+        constexpr int NF = NDB * NQB;          // fragments (4 values) per lane
+        constexpr int BLK = kBQ * D;           // partial elements per (split, tile) block
+        const int64_t grp = bh * a.nqt + qt;
+        auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
+        auto o_rsrc = [&](int sp) { return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, (int64_t)BLK * sizeof(PT)); };
+        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
+        auto e_rsrc = [&](int sp) { return make_rsrc(a.esc + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
+        auto frag_off = [&](int f) { return (((wid * NF + f) * 64 + lane) * 4) * (int)sizeof(PT); };
+        auto lse_off = [&](int qb) { return (wid * 32 + 16 * qb + n16) * 4; };
+        {
+            const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
+#pragma unroll
+            for (int qb = 0; qb < NQB; ++qb) {
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const f32x4 x = ov[qb][db] * inv[qb];
+                    if constexpr (sizeof(PT) == 4)
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), ors, frag_off(db * NQB + qb), 0, SC1);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2<PH>(x[0], x[1]), pack2<PH>(x[2], x[3])}, ors,
+                                                              frag_off(db * NQB + qb), 0, SC1);
+                }
+                if (g == 0) {
+                    const float lse = m[qb] + __builtin_amdgcn_logf(lsum[qb]);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse), lrs, lse_off(qb), 0, SC1);
+                    if constexpr (SCALED)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(esc[qb]), e_rsrc(split), lse_off(qb), 0, SC1);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* const last_flag = (int*)smem;  // LDS is free: the KV loop ended with a barrier
+        if (tid == 0) {
+            const unsigned old = __hip_atomic_fetch_add(a.counters + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old + 1 == (unsigned)a.nsplit;
+            if (last) a.counters[grp] = 0;  // leave the counter zero for the next launch
+            *last_flag = last;
+        }
+        __syncthreads();
+        if (!*last_flag) return;
+
+        // Sum in split order 0, 1, ... whatever workgroup came last (its own partial is read
+        // back too), so that O is bitwise repeatable.
+        const int ns = a.nsplit;
+        auto load_val = [&](int sp, int f) -> f32x4 {
+            if constexpr (sizeof(PT) == 4) {
+                return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(o_rsrc(sp), frag_off(f), 0, SC1));
+            } else {
+                const u32x2 u = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(o_rsrc(sp), frag_off(f), 0, SC1));
+                // (16-bit halves by shifts: hipcc miscompiles a bit_cast of u[1] to a 2 x bf16 vector
+                // into a second copy of u[0] and narrows the load to one dword)
+                f32x4 r;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const unsigned wd = u[j >> 1];
+                    r[j] = (float)__builtin_bit_cast(PH, (unsigned short)((j & 1) ? (wd >> 16) : (wd & 0xffff)));
+                }
+                return r;
+            }
+        };
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            float Mx = -INFINITY, E = -1000.f;
+            for (int sp = 0; sp < ns; ++sp) {
+                Mx = fmaxf(Mx, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1)));
+                if constexpr (SCALED)
+                    E = fmaxf(E, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1)));
+            }
+            f32x4 acc[NDB];
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
+            float wsum = 0.f;
+            for (int sp = 0; sp < ns; ++sp) {
+                const float wgt = __builtin_amdgcn_exp2f(
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1)) - Mx);
+                float wv = wgt;
+                if constexpr (SCALED) {
+                    const float es = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
+                    wv = __builtin_amdgcn_ldexpf(wgt, (int)(es - E));
+                }
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) acc[db] += wv * load_val(sp, db * NQB + qb);
+                wsum += wgt;
+            }
+            float inv_w = 1.f / wsum;
+            if constexpr (SCALED) {
+#pragma unroll
+                for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[db][i] = __builtin_amdgcn_ldexpf(acc[db][i] * inv_w, (int)E);
+                inv_w = 1.f;
+            }
+            const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
+            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o_final + (bh * a.Lq + q_row) * D, acc, inv_w);
         }
     }
 }
