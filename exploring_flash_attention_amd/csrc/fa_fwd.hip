@@ -5,9 +5,6 @@
 #include "fa_fwd_kernel.hpp"
 #include "fa_fwd16_kernel.hpp"
 
-#ifndef FA_SHAPE16
-#define FA_SHAPE16 1
-#endif
 
 namespace fa {
 
@@ -17,7 +14,9 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
-    if constexpr (FA_SHAPE16 && D == 128) {
+    // d = 128 without a key tail: the 16x16x32 kernel (fa_fwd16_kernel.hpp; C3 +5 %, C4 +3.4 %,
+    // the C5 partial pass +9 % over this file's 32x32x16 kernel)
+    if constexpr (D == 128) {
         if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {  // no key tail in any split
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();

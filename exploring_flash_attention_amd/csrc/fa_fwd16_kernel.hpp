@@ -52,36 +52,6 @@ __device__ __forceinline__ void quad_max2(float x0, float x1, float& m0, float& 
 template <typename X> struct TypeTag { using type = X; };
 
 
-#ifndef FA16_PIN
-#define FA16_PIN 1
-#endif
-#ifndef FA16_KA
-#define FA16_KA 3
-#endif
-#ifndef FA16_VA
-#define FA16_VA 2
-#endif
-#ifndef FA16_PV32
-#define FA16_PV32 0
-#endif
-#ifndef FA16_SPLIT
-#define FA16_SPLIT 0
-#endif
-#ifndef FA16_EXPA
-#define FA16_EXPA 28
-#endif
-
-// PV32 experiment: the phase-A slot that packs key block kb (the slot after its 8 exponentials),
-// or -1 when they end in phase B; and then the phase-B slot after them
-constexpr int cvt32_a(int kb) {
-    return 8 * (kb + 1) <= FA16_EXPA && (128 * (kb + 1) + FA16_EXPA - 1) / FA16_EXPA <= 15
-               ? (128 * (kb + 1) + FA16_EXPA - 1) / FA16_EXPA
-               : -1;
-}
-constexpr int cvt32_b(int kb) {
-    return cvt32_a(kb) >= 0 ? -1 : (8 * (kb + 1) - FA16_EXPA <= 0 ? 0 : (8 * (kb + 1) - FA16_EXPA + 1) / 2);
-}
-
 // MODE: kFinal (O), kPartial (normalised partial O + lse in row layout, fa_combine.hip reads
 // them) or kFused (partials in fragment order, combined by the last workgroup of each query
 // tile), as fa_fwd_kernel.hpp; every split a multiple of 64 keys and non-empty.
@@ -99,11 +69,12 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     constexpr int NDB = D / 16;        // 16-column blocks of O
     constexpr int NKK = kBK / 32;      // P.V k-steps (32 keys each)
     constexpr float kThr = 4.f;        // deferred rescale threshold (log2 units), as fa_fwd_kernel
-    constexpr int KA = FA16_KA, VA = FA16_VA;  // LDS reads in flight: K fragments, V^T operands
-    constexpr int EXPA = FA16_EXPA;            // exponentials in phase A (the rest: phase B, 2 per slot)
+    // Schedule constants, measured (A/B in one process): K fragments read
+    // KA slots ahead and V^T operands VA MFMA pairs ahead (2 / 4 and 1 / 3: within 0.5 %), EXPA of
+    // tile t's 32 exponentials in phase A (20 -> 28: +1 % at C3; 32: equal)
+    constexpr int KA = 3, VA = 2;  // LDS reads in flight: K fragments, V^T operands
+    constexpr int EXPA = 28;       // exponentials in phase A (the rest: phase B, 2 per slot)
     static_assert(EXPA >= 19 && EXPA <= 32, "key step 0 packs (phase A slots 6..13) follow their exponentials");
-    // experiment: P.V on 32x32x16 (final mode), P^T's lane groups exchanged by v_permlane16_swap
-    constexpr bool PV32 = FA16_PV32 && MODE == kFinal;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* const kring = smem;              // K ring: 2 slots
@@ -188,23 +159,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
                                             kOne | (kOne << 16)});
     }
     const float c = a.scale_log2;
-    // PV32 state: O^T as 32 dv x 32 query tiles (lane l: query l & 31, dv 32*db + 8*(i>>2) +
-    // 4*(l>>5) + (i&3)), row sums on 16x16x32 with the 0/1 selector (lane l: query (l&15) +
-    // 16*(l>>5)), V^T A operands from two transposed reads of 4 keys (rows 4*(l>>5) + (n>>2) and
-    // +8, columns 32*db + 16*((l>>4)&1) + 4*(n&3))
-    f32x16 o32[4];
-#pragma unroll
-    for (int db = 0; db < 4; ++db) o32[db] = f32x16{};
-    f32x4 ls16 = f32x4{};
-    v8 sel16;
-    {
-        constexpr unsigned kOne = std::is_same_v<T, __bf16> ? 0x3F80u : 0x3C00u;
-        const unsigned e = ((lane & 15) < 8) == (((lane >> 4) & 1) == 0) ? kOne | (kOne << 16) : 0u;
-        sel16 = __builtin_bit_cast(v8, u32x4{e, e, e, e});
-    }
-    const int r1 = 4 * (g >> 1) + (n16 >> 2), cb = 2 * (g & 1) + ((n16 >> 1) & 1);
-    const unsigned v32a = (unsigned)(size_t)vring + 64 * r1 + 16 * (cb ^ (g >> 1)) + 8 * (n16 & 1);
-    const unsigned v32b = (unsigned)(size_t)vring + 8 * ROWB + 64 * r1 + 16 * (cb ^ ((g >> 1) + 2)) + 8 * (n16 & 1);
 
     // (inline asm in nested generic lambdas must not capture: every operand is a parameter)
     auto kread_ = [](auto r_c, auto slot_c, u32x4 (&kf)[KA + 1], unsigned ka) {
@@ -225,22 +179,15 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
             asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][1]) : "v"(ve), "i"(OFF + 16 * ROWB) : "memory");
         }
     };
-    auto vread32_ = [](auto p_c, auto slot_c, u32x2 (&vf)[VA + 1][2], unsigned va, unsigned vb) {
-        constexpr int PP = decltype(p_c)::value, KB = PP / 4, DB = PP % 4, SL = decltype(slot_c)::value;
-        constexpr int OFF = SL * TILEB + KB * 16 * ROWB + 512 * DB;
-        static_assert(OFF + 8 * ROWB < 65536, "ds offset field is 16 bits");
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][0]) : "v"(va), "i"(OFF) : "memory");
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][1]) : "v"(vb), "i"(OFF) : "memory");
-    };
     auto lwait = [](auto n_c, u32x4& reg) {
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(reg) : "i"(decltype(n_c)::value) : "memory");
     };
     auto lwait2 = [](auto n_c, u32x2 (&reg)[2]) {
         asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(reg[0]), "+v"(reg[1]) : "i"(decltype(n_c)::value) : "memory");
     };
-    auto fence = [] {
-        if constexpr (FA16_PIN) __builtin_amdgcn_sched_barrier(0);
-    };
+    // closes an MFMA slot: hipcc keeps the slot's fillers with its MFMAs (the compiler-scheduled
+    // step measured -1.5 ... -2.5 %)
+    auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
 
     // S^T(t) of one tile from K slot SL: 16 K fragments, each feeding both query blocks
     auto qk_all = [&](auto slot_c, f32x4 (&s)[NKB][NQB]) {
@@ -293,25 +240,14 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         using SLN = std::integral_constant<int, 1 - P>;
         using SLC = std::integral_constant<int, P>;
         if (__builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
-            float alpha[NQB];
 #pragma unroll
             for (int qb = 0; qb < NQB; ++qb) {
                 const float m_new = fmaxf(m[qb], mx[qb]);
-                alpha[qb] = __builtin_amdgcn_exp2f(m[qb] - m_new);
+                const float alpha = __builtin_amdgcn_exp2f(m[qb] - m_new);
                 m[qb] = m_new;
-            }
-            if constexpr (PV32) {
-                const float ao = (lane >> 4) & 1 ? alpha[1] : alpha[0], al = lane >> 5 ? alpha[1] : alpha[0];
-                ls16 *= al;
+                rs[qb] *= alpha;
 #pragma unroll
-                for (int db = 0; db < 4; ++db) o32[db] *= ao;
-            } else {
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb) {
-                    rs[qb] *= alpha[qb];
-#pragma unroll
-                    for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha[qb];
-                }
+                for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
             }
         }
         const float nm0 = -m[0], nm1 = -m[1];
@@ -322,11 +258,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
 
         // score e of tile t: key step e / 16, query block (e / 8) & 1, key block 2*(e/16) + (e/4)&1, reg e&3
-        // (PV32: key block e / 8, query block (e / 4) & 1, reg e & 3: a key block's 8 scores first)
         auto ex = [&](auto e_c) {
-            constexpr int E = decltype(e_c)::value;
-            constexpr int KK = E / 16, QB = PV32 ? (E / 4) & 1 : (E / 8) & 1;
-            constexpr int KB = PV32 ? E / 8 : 2 * KK + ((E / 4) & 1), I = E & 3;
+            constexpr int E = decltype(e_c)::value, KK = E / 16, QB = (E / 8) & 1, KB = 2 * KK + ((E / 4) & 1), I = E & 3;
             sc[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, QB ? nm1 : nm0));
         };
         u32x4 pbu[NKK][NQB];  // packed P^T fragments
@@ -334,15 +267,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
             constexpr int K = decltype(k_c)::value, KK = K / 8, QB = (K / 4) & 1, J = K % 4;
             constexpr int KB = 2 * KK + (J >> 1), I = 2 * (J & 1);
             pbu[KK][QB][J] = pack2<T>(sc[KB][QB][I], sc[KB][QB][I + 1]);
-        };
-        u32x4 pb32[NKB];  // PV32: P^T of key block kb, query l & 31, keys 4*(l>>5) + {0..3, 8..11}
-        auto cvt32 = [&](auto kb_c) {
-            constexpr int KB = decltype(kb_c)::value;
-            const unsigned x0 = pack2<T>(sc[KB][0][0], sc[KB][0][1]), x1 = pack2<T>(sc[KB][0][2], sc[KB][0][3]);
-            const unsigned y0 = pack2<T>(sc[KB][1][0], sc[KB][1][1]), y1 = pack2<T>(sc[KB][1][2], sc[KB][1][3]);
-            const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-            pb32[KB] = u32x4{s0[0], s1[0], s0[1], s1[1]};
         };
         auto dma = [&](auto i_c) {
             constexpr int I = decltype(i_c)::value;
@@ -364,74 +288,25 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         }
         static_for<16>([&](auto s_c) {
             constexpr int S = decltype(s_c)::value;
-            constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;
             if constexpr (MORE) {
                 if constexpr (S + KA < 16) kread_(std::integral_constant<int, S + KA>{}, SLN{}, kf, kaddr);
                 constexpr int AFTER = (S + KA < 16 ? S + KA : 15) - S;
                 lwait(std::integral_constant<int, AFTER>{}, kf[S % (KA + 1)]);
-                sn[S % NKB][0] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[0][S / NKB], sn[S % NKB][0]);
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb)
+                    sn[S % NKB][qb] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[qb][S / NKB], sn[S % NKB][qb]);
             }
-            if constexpr (FA16_SPLIT && E1 > E0) ex(std::integral_constant<int, E0>{});
-            if constexpr (MORE && FA16_SPLIT) fence();
-            if constexpr (MORE)
-                sn[S % NKB][1] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[1][S / NKB], sn[S % NKB][1]);
-            constexpr int E0B = FA16_SPLIT && E1 > E0 ? E0 + 1 : E0;
-            static_for<E1 - E0B>([&](auto j_c) { ex(std::integral_constant<int, E0B + decltype(j_c)::value>{}); });
-            if constexpr (PV32) {
-                static_for<NKB>([&](auto kb_c) {
-                    constexpr int KB = decltype(kb_c)::value;
-                    if constexpr (cvt32_a(KB) == S) cvt32(kb_c);
-                });
-            } else if constexpr (S >= 6 && S < 14) {
-                cvt(std::integral_constant<int, S - 6>{});  // key step 0 packs
-            }
+            constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;
+            static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
+            if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key step 0 packs
             if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
             if constexpr (MORE) fence();
         });
 
         // ---- phase B: P.V(t) || exponentials of t (rest), row max of t+1
-        float m4[4];
-        auto rowmax_slot = [&](auto j_c) {  // row max of tile t+1 in slots 8..16
-            constexpr int J = decltype(j_c)::value;
-            if constexpr (MORE) {
-                if constexpr (J >= 8 && J < 16)
-                    chain_max(sn, std::integral_constant<int, (J - 8) / 2>{}, std::integral_constant<int, (J - 8) % 2>{},
-                              m4[(J - 8) / 2]);
-                if constexpr (J == 16) {
-                    quad_max2(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]), mx[0], mx[1]);
-                    mx[0] *= c;
-                    mx[1] *= c;
-                }
-            }
-        };
-        u32x2 vf[VA + 1][2];
-        if constexpr (PV32) {
-            // slot J: key block kb = J / 5; J % 5 < 4: P.V (32x32x16) of column block J % 5, 4: row sums
-            static_for<VA>([&](auto p_c) { vread32_(p_c, SLC{}, vf, v32a, v32b); });
-            static_for<20>([&](auto j_c) {
-                constexpr int J = decltype(j_c)::value;
-                constexpr int KB = J / 5, JJ = J % 5;
-                if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
-                if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
-                static_for<NKB>([&](auto kb_c) {
-                    if constexpr (cvt32_b(decltype(kb_c)::value) == J) cvt32(kb_c);
-                });
-                if constexpr (JJ < 4) {
-                    constexpr int PP = KB * 4 + JJ;
-                    if constexpr (PP + VA < 16) vread32_(std::integral_constant<int, PP + VA>{}, SLC{}, vf, v32a, v32b);
-                    constexpr int AFTER = 2 * ((PP + VA < 16 ? PP + VA : 15) - PP);
-                    lwait2(std::integral_constant<int, AFTER>{}, vf[PP % (VA + 1)]);
-                    const u32x4 vv = {vf[PP % (VA + 1)][0][0], vf[PP % (VA + 1)][0][1], vf[PP % (VA + 1)][1][0],
-                                      vf[PP % (VA + 1)][1][1]};
-                    o32[JJ] = M::mma(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pb32[KB]), o32[JJ]);
-                } else {
-                    ls16 = M::mma16(sel16, __builtin_bit_cast(v8, pb32[KB]), ls16);
-                }
-                rowmax_slot(j_c);
-                fence();
-            });
-        } else {
         // slot J: key step kk = J / 9; J % 9 < 8: P.V of column block J % 9, J % 9 == 8: row sums
+        u32x2 vf[VA + 1][2];
+        float m4[4];
         static_for<VA>([&](auto p_c) { vread_(p_c, SLC{}, vf, vb_e, vb_o); });
         static_for<18>([&](auto j_c) {
             constexpr int J = decltype(j_c)::value;
@@ -443,24 +318,30 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
                 lwait2(std::integral_constant<int, AFTER>{}, vf[PP % (VA + 1)]);
                 const u32x4 vv = {vf[PP % (VA + 1)][0][0], vf[PP % (VA + 1)][0][1], vf[PP % (VA + 1)][1][0],
                                   vf[PP % (VA + 1)][1][1]};
-                o[JJ][0] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[KK][0]), o[JJ][0]);
-                if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
-                if constexpr (FA16_SPLIT) fence();
-                o[JJ][1] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[KK][1]), o[JJ][1]);
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb)
+                    o[JJ][qb] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[KK][qb]), o[JJ][qb]);
             } else {
-                rs[0] = M::mma16(ones, __builtin_bit_cast(v8, pbu[KK][0]), rs[0]);
-                if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
-                if constexpr (FA16_SPLIT) fence();
-                rs[1] = M::mma16(ones, __builtin_bit_cast(v8, pbu[KK][1]), rs[1]);
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb) rs[qb] = M::mma16(ones, __builtin_bit_cast(v8, pbu[KK][qb]), rs[qb]);
             }
-            // exponentials EXPA..31, two per slot (one between the slot's MFMAs); key step 1
-            // packs in slots 1..8
+            // exponentials EXPA..31, two per slot; key step 1 packs in slots 1..8
+            if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
             if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
             if constexpr (J >= 1 && J <= 8) cvt(std::integral_constant<int, 8 + J - 1>{});
-            rowmax_slot(j_c);
+            if constexpr (MORE) {
+                // row max of tile t+1: chain (J - 8) / 2, half (J - 8) % 2 in slots 8..15
+                if constexpr (J >= 8 && J < 16)
+                    chain_max(sn, std::integral_constant<int, (J - 8) / 2>{}, std::integral_constant<int, (J - 8) % 2>{},
+                              m4[(J - 8) / 2]);
+                if constexpr (J == 16) {
+                    quad_max2(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]), mx[0], mx[1]);
+                    mx[0] *= c;
+                    mx[1] *= c;
+                }
+            }
             fence();
         });
-        }
         __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
     };
 
@@ -498,34 +379,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         } else {
             step(C0{}, LAST{}, t, sa, sb, mx);
         }
-    }
-
-    if constexpr (PV32) {
-        // lane l holds O^T[32*db + 8*(i>>2) + 4*hf + (i&3)][query l & 31]; the row sum of query
-        // q sits in lane (q < 16 ? q : q + 16); one v_permlane32_swap per dword pairs column
-        // groups into 16-byte stores (fa_fwd_kernel.hpp's store_row)
-        const int hf = lane >> 5;
-        const int rs16_src = ((lane & 31) < 16 ? (lane & 31) : (lane & 31) + 16) * 4;
-        const float l_tot = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(rs16_src, __builtin_bit_cast(int, ls16[0])));
-        const float inv = 1.f / l_tot;
-        const int64_t q_row = q_tile0 + wid * 32 + (lane & 31);
-        if (q_row < a.Lq) {
-            unsigned short* const Oh = (unsigned short*)a.o + (bh * a.Lq + q_row) * D;
-#pragma unroll
-            for (int db = 0; db < 4; ++db)
-#pragma unroll
-                for (int gp = 0; gp < 4; gp += 2) {
-                    const unsigned x0 = pack2<T>(o32[db][4 * gp + 0] * inv, o32[db][4 * gp + 1] * inv);
-                    const unsigned x1 = pack2<T>(o32[db][4 * gp + 2] * inv, o32[db][4 * gp + 3] * inv);
-                    const unsigned y0 = pack2<T>(o32[db][4 * gp + 4] * inv, o32[db][4 * gp + 5] * inv);
-                    const unsigned y1 = pack2<T>(o32[db][4 * gp + 6] * inv, o32[db][4 * gp + 7] * inv);
-                    const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-                    const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-                    const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
-                    *(u32x4*)(Oh + db * 32 + 8 * gp + 8 * hf) = u;
-                }
-        }
-        return;
     }
 
     // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n].  A 16-bit row is

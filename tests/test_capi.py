@@ -298,9 +298,10 @@ def test_product_build_carries_no_experiments():
     mk = open(os.path.join(csrc, "Makefile")).read()
     srcs = re.search(r"^SRCS\s*=\s*(.*)$", mk, flags=re.M).group(1).split()
     assert "fa_fwd_w64.hip" not in srcs
-    for f in srcs + ["fa_fwd_kernel.hpp", "fa_device.hpp", "fa_internal.hpp"]:
+    for f in srcs + ["fa_fwd_kernel.hpp", "fa_fwd16_kernel.hpp", "fa_device.hpp", "fa_internal.hpp"]:
         text = open(os.path.join(csrc, f)).read()
-        for knob in ("FA_ABL_", "FA_PP", "FA_SGB", "FA_QSPLIT", "FA_QSCALE", "FA_IGLP", "FA_W64", "getenv"):
+        for knob in ("FA_ABL_", "FA_PP", "FA_SGB", "FA_QSPLIT", "FA_QSCALE", "FA_IGLP", "FA_W64", "FA16_",
+                     "FA_SHAPE16", "getenv"):
             assert knob not in text, (f, knob)
     out = os.popen(f"nm -D --defined-only {L.LIB_PATH}").read()
     assert "fa_fwd_v1_w64" not in out and "fa_fwd_v2_ex" in out
