@@ -55,7 +55,9 @@ template <typename X> struct TypeTag { using type = X; };
 // MODE: kFinal (O), kPartial (normalised partial O + lse in row layout, fa_combine.hip reads
 // them) or kFused (partials in fragment order, combined by the last workgroup of each query
 // tile), as fa_fwd_kernel.hpp; every split a multiple of 64 keys and non-empty.
-template <typename T, typename PT, int D, int MODE>
+// QSTR: q is a strided view whose rows are contiguous (row stride d) -- the row ranges of the
+// multi-GPU partial path (fa_fwd_partial_ex); its heads are addressed through q_stride[0..1].
+template <typename T, typename PT, int D, int MODE, bool QSTR = false>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
@@ -94,7 +96,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     const int ntiles = (int)((kv_end - kv_begin) / kBK);
 
     const int64_t q_tile0 = (int64_t)qt * kBQ;
-    const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D + q_tile0 * D;
+    const int64_t q_head = QSTR ? (bh / a.H) * a.q_stride[0] + (bh % a.H) * a.q_stride[1] : bh * a.Lq * D;
+    const unsigned short* Qh = (const unsigned short*)a.q + q_head + q_tile0 * D;
     const int64_t q_rows = a.Lq - q_tile0 < kBQ ? a.Lq - q_tile0 : kBQ;
     const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, q_rows * ROWB);
     const unsigned short* const kbase = (const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D;

@@ -4,6 +4,7 @@
 // (FA-v1 fused / d-tiled), the fused split-KV mode (FA-v2) and the row-layout partial mode
 // (fa_fwd_partial_ex: one chunk of query rows per launch in the multi-GPU path).
 #include "fa_fwd_kernel.hpp"
+#include "fa_fwd16_kernel.hpp"
 
 namespace fa {
 
@@ -11,6 +12,15 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_strided_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
+    // the multi-GPU chunks at d = 128 (row ranges of q, contiguous K / V, whole 64-key tiles):
+    // the 16x16x32 kernel, as the contiguous partial launch, so both give the same bits
+    if constexpr (D == 128 && MODE == kPartial) {
+        const bool kv_contig = a.k_stride[2] == D && a.k_stride[1] == a.Lk * D && a.k_stride[0] == a.H * a.Lk * D;
+        if (kv_contig && a.q_stride[2] == D && a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {
+            hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
+            return hipGetLastError();
+        }
+    }
     if (a.Lk % bk_for(D))
         hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, true, true>), dim3((unsigned)nblk), dim3(kThreads),
                            lds, s, a);

@@ -483,10 +483,12 @@ def test_scaled_row_partials_beat_bf16(gpu):
 def test_dist_chunked_partials_match(gpu, pdtype):
     """The overlapped multi-GPU path computes the partials one destination chunk at a time
     from row-range views of q (fa_fwd_partial_ex, strided q): bitwise equal to the one-launch
-    partial kernel's all-to-all send layout, for W = 4 chunks (incl. a tail chunk length)."""
+    partial kernel's all-to-all send layout, for W = 4 chunks (incl. a tail chunk length) --
+    with a key tail, at d = 64, and C5's form (d = 128, whole 64-key tiles: the 16x16x32
+    kernel in both launches)."""
     from exploring_flash_attention_amd import dist as fdist
     from exploring_flash_attention_amd import ops
-    for (B, H, L, Lk, d) in ((2, 3, 512, 130, 128), (1, 2, 4 * 72, 64, 64)):
+    for (B, H, L, Lk, d) in ((2, 3, 512, 130, 128), (1, 2, 4 * 72, 64, 64), (2, 2, 4 * 96, 256, 128)):
         q, k, v = (x.to(gpu) for x in _inputs(B, H, L, d, torch.bfloat16, seed=41, Lk=Lk))
         W, Lc = 4, L // 4
         o_ref, lse_ref = ops.attention_partial(q, k, v, chunk_rows=Lc, partial_dtype=pdtype)
