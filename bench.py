@@ -195,6 +195,27 @@ def time_step(torch, step, steps, warmup, barrier):
     return wall, ev0.elapsed_time(ev1)
 
 
+def fwd_kernel_name(d, Lk, what):
+    """The kernel a contiguous forward launch runs (fa_fwd.hip launch_one): d = 128 with whole
+    64-key tiles on fa_fwd16_kernel (16x16x32 MFMA), everything else on fa_fwd_kernel."""
+    name = "fa_fwd16_kernel" if d == 128 and Lk % 64 == 0 else "fa_fwd_kernel"
+    return f"{name} ({what})"
+
+
+def clock_settle(torch, step, seconds):
+    """Run `step` untimed, back to back, for about `seconds` (the MI355X clock ramps over the
+    first ~50 ms of sustained work); returns the seconds spent."""
+    if seconds <= 0:
+        return 0.0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            step()
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
 def c5_step(torch, fdist, dev, world, rank, impl="torch"):
     """One C5 split-KV step closure: the keys of B=32 H=8 L=16384 d=128 sharded over the
     ranks, partial kernel -> all-to-all -> combine (dist.splitkv_attention)."""
@@ -208,12 +229,14 @@ def c5_step(torch, fdist, dev, world, rank, impl="torch"):
 
         def step():
             fdist.splitkv_attention_native(q, k, v, comm)
-        kernel = "fa_fwd_kernel (partial) + RCCL send/recv + fa_combine_kernel (C ABI)"
+        kernel = (fwd_kernel_name(d, hi - lo, "partial, one launch per destination chunk") +
+                  " + RCCL send/recv on the exchange stream + fa_combine_kernel (C ABI fa_fwd_v2_dist)")
     else:
         def step():
             fdist.splitkv_attention(q, k, v)
-        kernel = ("fa_fwd_kernel (partial, one launch per destination chunk) + pipelined RCCL send/recv + "
-                  "fa_combine_kernel" if world > 1 else "fa_fwd_kernel (partial) + fa_combine_kernel")
+        kernel = (fwd_kernel_name(d, hi - lo, "partial, one launch per destination chunk") +
+                  " + pipelined RCCL send/recv + fa_combine_kernel" if world > 1
+                  else fwd_kernel_name(d, hi - lo, "partial") + " + fa_combine_kernel")
     return step, kernel, flops(B, H, L, d, Lk=hi - lo)
 
 
@@ -352,6 +375,23 @@ def output_check(torch, q, k, v, out, n=16):
             "reference": "torch fp64 softmax(q k^T / sqrt(d)) v on the device, sampled heads incl. first/last"}
 
 
+def splitkv_scaling_field(c5, world):
+    """The north_star's multi-GPU row (C5: one L=16384 batch's keys sharded over the ranks,
+    partials exchanged over RCCL, combined per rank) lifted to the top of the line, so that the
+    driver's 1/2/4/8-GPU runs record the split-KV curve beside the heads-parallel headline."""
+    rec = {"config": "C5: B=32 H=8 L=16384 d=128 bf16, keys sharded over the ranks", "ranks": world,
+           "unit": "GFLOP/s (whole job)"}
+    if "error" in c5:
+        rec["error"] = c5["error"]
+        return rec
+    bd = c5.get("breakdown_max_over_ranks", {})
+    rec.update(ms=c5["ms"], value=round(c5["tflops"] * 1e3, 1), frac=c5["frac"], exchange=c5.get("exchange"))
+    for key in ("partial_ms", "combine_ms", "exchange_ms", "exchange_gbps", "exchange_bytes_per_rank"):
+        if key in bd:
+            rec[key] = bd[key]
+    return rec
+
+
 WATCHDOG_EXIT = 3
 
 
@@ -419,8 +459,8 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0, help="CPU baseline pool size (0 = the usable host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the per-variant extra timings")
-    ap.add_argument("--clock-warmup", type=float, default=0.1,
-                    help="seconds of untimed forwards before any timing (clock settle; 0 = off)")
+    ap.add_argument("--clock-warmup", type=float, default=0.25,
+                    help="seconds of untimed headline steps right before --warmup (clock settle; 0 = off)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -461,24 +501,13 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # Clock settle: the chip needs ~50 ms of back-to-back work before its clock holds (DESIGN.md
-    # section 5), so ~0.1 s of untimed C3 forwards run first (reported as clock_warmup_s); the
-    # headline then still times exactly --steps launches after exactly --warmup more.
-    t_warm = 0.0
-    if args.mode == "heads" and args.clock_warmup > 0:
-        cw = CONFIGS["c3"]
-        qw, kw, vw = _make_inputs(torch, dev, cw["B"], cw["H"], cw["L"], cw["d"], seed=3)
-        torch.cuda.synchronize()
-        t0w = time.perf_counter()
-        while time.perf_counter() - t0w < args.clock_warmup:
-            for _ in range(50):
-                ops.attention_v1(qw, kw, vw)
-            torch.cuda.synchronize()
-        t_warm = time.perf_counter() - t0w
-        del qw, kw, vw
-
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra and args.mode == "heads":
+        # the extras get a settled clock too (C3 forwards, untimed), then each its own warm-up
+        cw = CONFIGS["c3"]
+        qw, kw, vw = _make_inputs(torch, dev, cw["B"], cw["H"], cw["L"], cw["d"], seed=3)
+        clock_settle(torch, lambda: ops.attention_v1(qw, kw, vw), 0.1)
+        del qw, kw, vw
         # per-variant timings at N=1 (informational; not the headline value).  They run
         # before the headline, so the headline's window also finds the clock settled.
         # (C3's tiled-d form is the same launch as the headline: fa_fwd_v1_tiled_d validates
@@ -487,14 +516,14 @@ def main():
         torch.cuda.empty_cache()
 
     check = None
+    t_warm = 0.0
     if args.mode == "heads":
         q, k, v = _make_inputs(torch, dev, B, H, L, d, seed=1234 + rank)
         out = torch.empty_like(q)
         if cfg["variant"] == "v1":
             def step():
                 ops.attention_v1(q, k, v, out=out)
-            kernel = ("fa_fwd16_kernel (final, 16x16x32 MFMA)" if d == 128 and L % 64 == 0
-                      else "fa_fwd_kernel (final)")
+            kernel = fwd_kernel_name(d, L, "final")
         else:
             nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -502,9 +531,15 @@ def main():
             def step():
                 ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
             _, _, ppt = ops.v2_split_plan(B, H, L, d, cfg["kvtpb"], q.dtype)
-            kernel = ("fa_fwd_kernel (split-KV, in-kernel combine)" if ppt > 1
-                      else "fa_fwd16_kernel (final: the library groups every key block of a query tile "
-                           "on one workgroup, fa_fwd_v2_split_plan)")
+            kernel = (fwd_kernel_name(d, L, "fused split-KV, in-kernel combine") if ppt > 1
+                      else fwd_kernel_name(d, L, "final: the library groups every key block of a query tile "
+                                                 "on one workgroup, fa_fwd_v2_split_plan"))
+        # Clock settle, immediately before the headline's --warmup (after the extras, whose
+        # last shapes are small): the chip needs ~50 ms of back-to-back work before its clock
+        # holds, so the headline's own step runs untimed for
+        # --clock-warmup seconds (reported as clock_warmup_s); then exactly --warmup more
+        # untimed steps and exactly --steps timed ones.
+        t_warm = clock_settle(torch, step, args.clock_warmup)
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         work = flops(B, H, L, d)
         workload = ("FA-v1 fused / tiled-d forward (one kernel)" if cfg["variant"] == "v1"
@@ -515,6 +550,7 @@ def main():
     else:
         # C5: keys of one L=16384 sequence sharded over the ranks; all-to-all combine.
         step, kernel, work = c5_step(torch, fdist, dev, world, rank, args.dist_impl)  # work: this rank's share
+        t_warm = clock_settle(torch, step, min(args.clock_warmup, 0.1))
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
         workload = "FA-v2 split-KV forward, keys sharded over ranks"
         parallel = f"kv{world}"
@@ -607,6 +643,8 @@ def main():
     if rank == 0:
         if extra:
             line["extra"] = extra
+        if "c5_splitkv_dist" in extra:
+            line["splitkv_scaling"] = splitkv_scaling_field(extra["c5_splitkv_dist"], world)
         print(json.dumps(line), flush=True)
         printed = True
     if dog is not None:

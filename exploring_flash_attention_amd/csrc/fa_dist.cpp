@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/fa_mi355x_dist.h"
+#include "fa_dist_schedule.hpp"
 
 static_assert(sizeof(ncclUniqueId) == FA_DIST_UNIQUE_ID_BYTES, "ncclUniqueId size");
 
@@ -47,7 +48,7 @@ struct Comm {
     int world = 0, rank = 0, device = 0;
     hipStream_t xstream = nullptr;
     std::vector<hipEvent_t> ev;  // ev[s], s = 1..world-1: partial of step s queued; ev[0]: exchange done
-    bool broken = false;         // an RCCL enqueue failed after others were posted
+    bool broken = false;         // a call failed after its first exchange step was posted
 };
 
 void destroy(Comm* c) {
@@ -83,6 +84,68 @@ Layout layout(int64_t BH, int64_t L, int64_t d, int dtype, int pdtype) {
     w.total = w.gather + align256(rows * d * esize(dtype));
     return w;
 }
+
+
+// The HIP / RCCL operations of fa_dist_schedule.hpp's run_exchange for one call.
+struct RcclOps {
+    Comm* c;
+    char* ws;
+    const void *q, *k, *v;
+    int64_t B, H, L, Lc, d;
+    int dtype, pdtype;
+    hipStream_t s;
+    int partial_chunk(int p, size_t o_off, size_t l_off) {
+        // a q row-range view in place: rows [p*Lc, (p+1)*Lc) of every head
+        const int64_t qst[3] = {H * L * d, L * d, d};
+        const char* qp = (const char*)q + (size_t)p * Lc * d * esize(dtype);
+        if (int st = fa_fwd_partial_ex(qp, k, v, ws + o_off, ws + l_off, B, H, Lc, Lc, d, Lc, qst, dtype, pdtype, s))
+            return core_fail(st, "fa_fwd_partial_ex");
+        return FA_OK;
+    }
+    int partial_all(size_t o_off, size_t l_off) {
+        if (int st = fa_fwd_partial(q, k, v, ws + o_off, ws + l_off, B, H, L, Lc, d, Lc, dtype, pdtype, s))
+            return core_fail(st, "fa_fwd_partial");
+        return FA_OK;
+    }
+    int fence_to_exchange(int ev) {
+        if (hipError_t he = hipEventRecord(c->ev[ev], s)) return hip_fail(he, "hipEventRecord");
+        if (hipError_t he = hipStreamWaitEvent(c->xstream, c->ev[ev], 0)) return hip_fail(he, "hipStreamWaitEvent");
+        return FA_OK;
+    }
+    int fence_to_compute() {
+        if (hipError_t he = hipEventRecord(c->ev[0], c->xstream)) return hip_fail(he, "hipEventRecord");
+        if (hipError_t he = hipStreamWaitEvent(s, c->ev[0], 0)) return hip_fail(he, "hipStreamWaitEvent");
+        return FA_OK;
+    }
+    // one step of the shifted exchange on the exchange stream: send chunk rank+st to rank+st,
+    // receive chunk rank from rank-st (all ranks' links busy at once, every step a matching)
+    int post_step(int st, int dst, int src, size_t so, size_t ro, size_t sl, size_t rl) {
+        const size_t chunk_o = (size_t)B * H * Lc * d * esize(pdtype);
+        const size_t chunk_l = (size_t)B * H * Lc * lsize(dtype, pdtype);
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess) {
+            // (inside a group RCCL only queues; an error here discards the whole group at
+            // ncclGroupEnd, nothing of it is posted)
+            ncclResult_t e = ncclSend(ws + so, chunk_o, ncclUint8, dst, c->nccl, c->xstream);
+            if (e == ncclSuccess) e = ncclRecv(ws + ro, chunk_o, ncclUint8, src, c->nccl, c->xstream);
+            if (e == ncclSuccess) e = ncclSend(ws + sl, chunk_l, ncclUint8, dst, c->nccl, c->xstream);
+            if (e == ncclSuccess) e = ncclRecv(ws + rl, chunk_l, ncclUint8, src, c->nccl, c->xstream);
+            r = ncclGroupEnd();
+            if (e != ncclSuccess) r = e;
+        }
+        if (r != ncclSuccess) {
+            char what[96];
+            snprintf(what, sizeof what, "exchange step %d (to rank %d, from rank %d)", st, dst, src);
+            return rccl_fail(r, what);
+        }
+        return FA_OK;
+    }
+    int local_copy(size_t dst_off, size_t src_off, size_t bytes) {
+        if (hipError_t he = hipMemcpyAsync(ws + dst_off, ws + src_off, bytes, hipMemcpyDeviceToDevice, s))
+            return hip_fail(he, "own chunk copy");
+        return FA_OK;
+    }
+};
 
 }  // namespace
 
@@ -181,86 +244,37 @@ int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void
     // pipelined (one partial launch per destination chunk, a q row-range view in place) for
     // bf16 / fp16; fp64 (no strided kernels) computes all chunks in one launch first
     const bool pipelined = dtype != FA_DTYPE_FP64 && world > 1 && d % 8 == 0;
-    const int64_t qst[3] = {H * L * d, L * d, d};
-    const size_t qrow_bytes = (size_t)d * esize(dtype);
-    auto partial_chunk = [&](int p, char* o_dst, char* l_dst) {
-        return fa_fwd_partial_ex((const char*)q + (size_t)p * Lc * qrow_bytes, k_shard, v_shard, o_dst, l_dst, B, H,
-                                 Lc, Lc, d, Lc, qst, dtype, partial_dtype, stream);
-    };
-    // one step of the shifted exchange on the exchange stream: send chunk rank+st to rank+st,
-    // receive chunk rank from rank-st (all ranks' links busy at once, every step a matching)
-    auto post_step = [&](int st) -> int {
-        const int dst = (rank + st) % world, src = (rank - st + world) % world;
-        ncclResult_t r = ncclGroupStart();
-        if (r == ncclSuccess) {
-            // (inside a group RCCL only queues; an error here discards the whole group at
-            // ncclGroupEnd, nothing of it is posted)
-            ncclResult_t e = ncclSend(ws + w.send_o + dst * chunk_o, chunk_o, ncclUint8, dst, c->nccl, c->xstream);
-            if (e == ncclSuccess) e = ncclRecv(ws + w.recv_o + src * chunk_o, chunk_o, ncclUint8, src, c->nccl, c->xstream);
-            if (e == ncclSuccess) e = ncclSend(ws + w.send_lse + dst * chunk_l, chunk_l, ncclUint8, dst, c->nccl, c->xstream);
-            if (e == ncclSuccess) e = ncclRecv(ws + w.recv_lse + src * chunk_l, chunk_l, ncclUint8, src, c->nccl, c->xstream);
-            r = ncclGroupEnd();
-            if (e != ncclSuccess) r = e;
-        }
-        if (r != ncclSuccess) {
-            if (st > 1) c->broken = true;  // earlier steps are posted: the peers are mid-exchange
-            char what[96];
-            snprintf(what, sizeof what, "exchange step %d (to rank %d, from rank %d)", st, dst, src);
-            return rccl_fail(r, what);
-        }
-        return FA_OK;
-    };
-
-    if (world == 1) {  // nothing to exchange: partial straight into the receive side
-        if (int st = fa_fwd_partial(q, k_shard, v_shard, ws + w.recv_o, ws + w.recv_lse, B, H, L, Lc, d, Lc, dtype,
-                                    partial_dtype, stream))
-            return core_fail(st, "fa_fwd_partial");
-    } else if (pipelined) {
-        for (int st = 1; st < world; ++st) {
-            const int dst = (rank + st) % world;
-            if (int e = partial_chunk(dst, ws + w.send_o + dst * chunk_o, ws + w.send_lse + dst * chunk_l)) {
-                if (st > 1) c->broken = true;
-                return core_fail(e, "fa_fwd_partial_ex");
-            }
-            if (hipError_t he = hipEventRecord(c->ev[st], s)) return hip_fail(he, "hipEventRecord");
-            if (hipError_t he = hipStreamWaitEvent(c->xstream, c->ev[st], 0)) return hip_fail(he, "hipStreamWaitEvent");
-            if (int e = post_step(st)) return e;
-        }
-        // own chunk last, straight into the receive buffer (it never crosses a link)
-        if (int e = partial_chunk(rank, ws + w.recv_o + rank * chunk_o, ws + w.recv_lse + rank * chunk_l)) {
-            c->broken = true;
-            return core_fail(e, "fa_fwd_partial_ex");
-        }
-    } else {
-        // all chunks in one launch (send layout), then the W-1 steps; the own chunk is a local copy
-        if (int st = fa_fwd_partial(q, k_shard, v_shard, ws + w.send_o, ws + w.send_lse, B, H, L, Lc, d, Lc, dtype,
-                                    partial_dtype, stream))
-            return core_fail(st, "fa_fwd_partial");
-        if (hipError_t he = hipEventRecord(c->ev[1], s)) return hip_fail(he, "hipEventRecord");
-        if (hipError_t he = hipStreamWaitEvent(c->xstream, c->ev[1], 0)) return hip_fail(he, "hipStreamWaitEvent");
-        for (int st = 1; st < world; ++st)
-            if (int e = post_step(st)) return e;
-        if (hipError_t he = hipMemcpyAsync(ws + w.recv_o + rank * chunk_o, ws + w.send_o + rank * chunk_o, chunk_o,
-                                           hipMemcpyDeviceToDevice, s))
-            return hip_fail(he, "own chunk copy");
-        if (hipError_t he = hipMemcpyAsync(ws + w.recv_lse + rank * chunk_l, ws + w.send_lse + rank * chunk_l,
-                                           chunk_l, hipMemcpyDeviceToDevice, s))
-            return hip_fail(he, "own chunk copy");
-    }
-    if (world > 1) {  // the combine waits for the exchange
-        if (hipError_t he = hipEventRecord(c->ev[0], c->xstream)) return hip_fail(he, "hipEventRecord");
-        if (hipError_t he = hipStreamWaitEvent(s, c->ev[0], 0)) return hip_fail(he, "hipStreamWaitEvent");
-    }
+    // The schedule (step pairing, chunk offsets, own-chunk path, failure latch) is
+    // fa_dist_schedule.hpp's run_exchange, exercised on the CPU with an in-process transport
+    // (tests/test_dist_schedule.py); these are its HIP / RCCL operations.
+    fa::dist::Plan plan;
+    plan.world = world;
+    plan.rank = rank;
+    plan.pipelined = pipelined;
+    plan.send_o = w.send_o;
+    plan.send_lse = w.send_lse;
+    plan.recv_o = w.recv_o;
+    plan.recv_lse = w.recv_lse;
+    plan.chunk_o = chunk_o;
+    plan.chunk_l = chunk_l;
+    RcclOps ops{c, ws, q, k_shard, v_shard, B, H, L, Lc, d, dtype, partial_dtype, s};
+    if (int st = fa::dist::run_exchange(plan, ops, c->broken)) return st;
     // combine the W partials of this rank's rows
     void* rows_out = gather && world > 1 ? (void*)(ws + w.gather + rank * (size_t)BH * Lc * d * esize(dtype)) : o;
+    const bool gathering = gather && world > 1;  // peers will post the all-gather: a failure
+                                                   // from here on leaves them waiting on it
     if (int st = fa_combine(ws + w.recv_o, ws + w.recv_lse, rows_out, world, B, H, Lc, d, dtype, partial_dtype,
-                            stream))
+                            stream)) {
+        if (gathering) c->broken = true;
         return core_fail(st, "fa_combine");
-    if (!gather || world == 1) return ok();
+    }
+    if (!gathering) return ok();
     // all-gather [W][B*H][Lc][d] then the strided copy to [B*H][W*Lc][d]
     const size_t part = (size_t)BH * Lc * d * esize(dtype);
-    if (ncclResult_t r = ncclAllGather(ws + w.gather + rank * part, ws + w.gather, part, ncclUint8, c->nccl, s))
+    if (ncclResult_t r = ncclAllGather(ws + w.gather + rank * part, ws + w.gather, part, ncclUint8, c->nccl, s)) {
+        c->broken = true;
         return rccl_fail(r, "ncclAllGather");
+    }
     const size_t row_bytes = (size_t)Lc * d * esize(dtype);
     for (int p = 0; p < world; ++p)
         if (hipError_t he = hipMemcpy2DAsync((char*)o + p * row_bytes, (size_t)L * d * esize(dtype),

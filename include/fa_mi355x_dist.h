@@ -61,9 +61,12 @@ int fa_fwd_v2_dist_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d, in
  * [B, H, L/W, d] of O, or the full [B, H, L, d] O when gather != 0.  Asynchronous on
  * `stream`: the kernels and the all-gather run on it, the send/recv steps on the handle's
  * exchange stream, ordered against it by events.  Every argument is checked before anything
- * is enqueued (a call that returns an error has posted nothing to the peers); the one failure
- * that can still strike part-way -- an RCCL enqueue error after earlier steps were posted --
- * returns FA_ERR_RCCL and marks the handle unusable (later calls refuse; destroy it). */
+ * is enqueued (a call that returns an error has posted nothing to the peers).  A failure that
+ * strikes after the first exchange step was posted -- a kernel launch, an event record or
+ * wait, a later step's RCCL enqueue, or, with gather, the combine or the all-gather -- leaves
+ * the peers waiting on posts this rank will never make: it returns the error and marks the
+ * handle unusable (later calls refuse with FA_ERR_RCCL; destroy it).  The schedule and this
+ * latch are csrc/fa_dist_schedule.hpp, tested on the CPU with an in-process transport. */
 int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void* o,
                    int64_t B, int64_t H, int64_t L, int64_t d, void* comm, int gather,
                    void* workspace, size_t workspace_bytes, int dtype, int partial_dtype,

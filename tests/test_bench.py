@@ -85,3 +85,26 @@ def test_extra_shapes_split_where_the_library_splits():
         _, B, H, L, d, _, kvt, grp = shapes[base + "_unsplit"]
         blocks = ops.v2_split_plan(B, H, L, d, kvt)[0]
         assert grp == "all" and ops.v2_split_plan(B, H, L, d, kvt, blocks_per_workgroup=blocks)[2] == 1
+
+
+def test_splitkv_scaling_field_at_mocked_two_ranks():
+    """At N > 1 the C5 split-KV measurement (north_star's multi-GPU row) is a top-level field of
+    the bench line, carrying ms, whole-job rate, frac and the exchange's own ms / GB/s."""
+    sys.path.insert(0, ROOT)
+    import bench
+    c5 = {"ms": 15.0, "tflops": 2345.6, "frac": 0.469, "ranks": 2, "exchange": "pairwise send/recv",
+          "breakdown_max_over_ranks": {"partial_ms": 14.1, "combine_ms": 0.4, "exchange_ms": 3.2,
+                                       "exchange_gbps": 167.8, "exchange_bytes_per_rank": 537_000_000}}
+    rec = bench.splitkv_scaling_field(c5, 2)
+    assert rec["ranks"] == 2 and rec["ms"] == 15.0 and rec["frac"] == 0.469
+    assert rec["value"] == 2345600.0 and rec["exchange_ms"] == 3.2 and rec["exchange_gbps"] == 167.8
+    err = bench.splitkv_scaling_field({"error": "no result within 240 s", "ranks": 2}, 2)
+    assert err["error"].startswith("no result") and "ms" not in err
+
+
+def test_kernel_labels_follow_the_dispatch():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.fwd_kernel_name(128, 1024, "final").startswith("fa_fwd16_kernel")
+    assert bench.fwd_kernel_name(128, 1000, "final").startswith("fa_fwd_kernel")
+    assert bench.fwd_kernel_name(32, 1024, "final").startswith("fa_fwd_kernel")
