@@ -41,6 +41,7 @@ SIGNATURES = {
     "fa_fwd_v1_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, ctypes.c_double, _I, _P]),
     "fa_fwd_v1_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, ctypes.c_double, _I, _P]),
     "fa_fwd_v1_tiled_d": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _P]),
+    "fa_fwd_v1_tiled_d_scaled": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, ctypes.c_double, _I, _P]),
     "fa_fwd_v2_split_plan": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I, _PI, _PI, _PI]),
     "fa_fwd_v2_workspace_size": (_I, [_I64, _I64, _I64, _I64, _I, _I, _I,
                                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_I)]),

@@ -36,6 +36,11 @@ int ok() {
 }
 
 bool supported_d(int64_t d) { return d == 32 || d == 64 || d == 128 || d == 256; }
+// head dims past one tile: the d-tiled kernels (fa_fwd_dtiled.hip, fa_fwd64.hip), final mode only
+bool wide_d(int64_t d) { return d == 384 || d == 512; }
+// a d tile as the d-tiled kernels take it: 32, 64 or 128 columns (the request rounded down to
+// one of them, at least 32: a QK^T k-step is 32 columns; all three divide 384 and 512)
+int dtile_eff(int dt) { return dt >= 128 ? 128 : dt >= 64 ? 64 : 32; }
 
 int check_dtype(int dtype, fa::Elem* e) {
     if (dtype == FA_DTYPE_BF16) { *e = fa::Elem::BF16; return FA_OK; }
@@ -57,16 +62,16 @@ int check_partial_dtype(int pdtype, int dtype, fa::Elem* e) {
                 "partial dtype %d must be FA_DTYPE_FP32, FA_DTYPE_FP16_SCALED or the input dtype %d", pdtype, dtype);
 }
 
-int check_shape(int64_t B, int64_t H, int64_t L, int64_t d) {
+int check_shape(int64_t B, int64_t H, int64_t L, int64_t d, bool wide = false) {
     if (B <= 0 || H <= 0 || L <= 0 || d <= 0)
         return fail(FA_ERR_INVALID_ARG, "all dimensions must be positive (B=%lld H=%lld L=%lld d=%lld)",
                     (long long)B, (long long)H, (long long)L, (long long)d);
-    if (!supported_d(d))
-        return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel (supported: 32, 64, 128, 256)",
-                    (long long)d);
+    if (!supported_d(d) && !(wide && wide_d(d)))
+        return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel here (supported: 32, 64, 128, 256%s)",
+                    (long long)d, wide ? ", 384, 512" : "; 384 and 512 through the FA-v1 / tiled-d / unsplit v2 paths");
     if (L > (int64_t)1 << 30)
         return fail(FA_ERR_UNSUPPORTED, "L=%lld exceeds 2^30", (long long)L);
-    const int64_t nqt = (L + fa::kBQ - 1) / fa::kBQ;
+    const int64_t nqt = (L + 63) / 64;  // the smallest query tile of any kernel
     if (B * H * nqt > (int64_t)0x7fffffff)
         return fail(FA_ERR_UNSUPPORTED, "grid of %lld workgroups exceeds 2^31-1", (long long)(B * H * nqt));
     return FA_OK;
@@ -90,10 +95,14 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(FA_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-// query rows per workgroup and keys per KV tile of the kernel serving dtype e
-int rows_per_block(fa::Elem e) { return e == fa::Elem::F64 ? fa::fwd64_rows_per_block() : fa::kBQ; }
+// query rows per workgroup and keys per KV tile of the kernel serving dtype e (and head dim d)
+int rows_per_block(fa::Elem e, int64_t d = 128) {
+    if (wide_d(d)) return fa::dtiled_rows_per_block();
+    return e == fa::Elem::F64 ? fa::fwd64_rows_per_block() : fa::kBQ;
+}
 int keys_per_tile(fa::Elem e, int64_t d) {
-    return e == fa::Elem::F64 ? fa::fwd64_keys_per_tile() : fa::bk_for((int)d);
+    if (e == fa::Elem::F64) return fa::fwd64_keys_per_tile();
+    return wide_d(d) ? 64 : fa::bk_for((int)d);
 }
 
 fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int64_t BH,
@@ -101,7 +110,7 @@ fa::FwdArgs base_args(const void* q, const void* k, const void* v, void* o, int6
     fa::FwdArgs a{};
     a.q = q; a.k = k; a.v = v; a.o = o; a.lse = nullptr;
     a.BH = BH; a.Lq = Lq; a.Lk = Lk;
-    a.nqt = (int)((Lq + rows_per_block(e) - 1) / rows_per_block(e));
+    a.nqt = (int)((Lq + rows_per_block(e, d) - 1) / rows_per_block(e, d));
     a.scale_log2_64 = 1.4426950408889634 / std::sqrt((double)d);
     a.nsplit = 1;
     a.kv_per_split = (int)Lk;
@@ -155,7 +164,18 @@ int apply_scale(fa::FwdArgs& a, double softmax_scale) {
     return FA_OK;
 }
 
+// d = 384 / 512: the d-tiled kernels with the given (requested) d tiles; their query tile is
+// 64 rows (dtiled_rows_per_block; the fp64 kernel's too)
+hipError_t launch_wide(fa::Elem e, int d, fa::FwdArgs a, int d_tile_qk, int d_tile_v, hipStream_t s) {
+    a.nqt = (int)((a.Lq + fa::dtiled_rows_per_block() - 1) / fa::dtiled_rows_per_block());
+    a.d_tile_qk = dtile_eff(d_tile_qk);
+    a.d_tile_v = dtile_eff(d_tile_v);
+    return e == fa::Elem::F64 ? fa::launch_fwd64_dtiled(d, a, s) : fa::launch_fwd_dtiled(e, d, a, s);
+}
+
+// final mode; wide head dims take the d-tiled kernels with their largest tiles
 hipError_t launch_final(fa::Elem e, int d, const fa::FwdArgs& a, hipStream_t s) {
+    if (wide_d(d)) return launch_wide(e, d, a, 128, 128, s);
     return e == fa::Elem::F64 ? fa::launch_fwd64(d, fa::kFinal, a, s) : fa::launch_fwd(e, e, d, fa::kFinal, a, s);
 }
 
@@ -224,10 +244,10 @@ int64_t wanted_partials(int64_t items, int64_t cap) {
 // FA_KV_TILES_AUTO: pick the split from occupancy: the KV tiles of a head
 // cut into wanted_partials() equal splits.
 int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
-    if (BH <= 0 || L <= 0 || !supported_d(d)) return 1;  // the shape checks report these
+    if (BH <= 0 || L <= 0 || !(supported_d(d) || wide_d(d))) return 1;  // the shape checks report these
     const int64_t bk = keys_per_tile(e, d);
     const int64_t ntiles = (L + bk - 1) / bk;
-    const int64_t items = BH * ((L + rows_per_block(e) - 1) / rows_per_block(e));
+    const int64_t items = BH * ((L + rows_per_block(e, d) - 1) / rows_per_block(e, d));
     const int64_t ns = wanted_partials(items, ntiles);
     return (int)((ntiles + ns - 1) / ns);
 }
@@ -261,9 +281,11 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
     p.kvtpb = kvtpb;
     const int64_t keys = (int64_t)kvtpb * keys_per_tile(e, d);
     p.units = (int)((L + keys - 1) / keys);
-    const int64_t items = BH * ((L + rows_per_block(e) - 1) / rows_per_block(e));
+    const int64_t items = BH * ((L + rows_per_block(e, d) - 1) / rows_per_block(e, d));
     p.group = 1;
-    if (blocks_per_wg > 0) {
+    if (wide_d(d)) {
+        p.group = p.units;  // d = 384 / 512: no split kernel -- every key block on one workgroup
+    } else if (blocks_per_wg > 0) {
         p.group = blocks_per_wg < p.units ? blocks_per_wg : p.units;
     } else {
         const int64_t ns = wanted_partials(items, p.units);
@@ -282,7 +304,7 @@ int v2_workspace(int64_t B, int64_t H, int64_t L, int64_t d, const SplitPlan& sp
     const int ns = sp.launched;
     // one workgroup per (query tile, split group, b*h): the grid and the kernel's block index
     // are 32-bit (dim3, xcd_remap), so a grid past 2^31-1 is refused instead of truncated
-    const int64_t nqt = (L + rows_per_block(e) - 1) / rows_per_block(e);
+    const int64_t nqt = (L + rows_per_block(e, d) - 1) / rows_per_block(e, d);
     if (B * H * nqt > (int64_t)0x7fffffff / ns)
         return fail(FA_ERR_UNSUPPORTED, "split-KV grid of %lld x %d workgroups exceeds 2^31-1 "
                     "(raise kv_tiles_per_block)", (long long)(B * H * nqt), ns);
@@ -295,15 +317,22 @@ int v2_workspace(int64_t B, int64_t H, int64_t L, int64_t d, const SplitPlan& sp
 
 extern "C" {
 
-int fa_version(void) { return (0 << 16) | (1 << 8) | 0; }
+int fa_version(void) { return (FA_MI355X_VERSION_MAJOR << 16) | (FA_MI355X_VERSION_MINOR << 8) | 0; }
 
 const char* fa_last_error(void) { return g_err.c_str(); }
 
 int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int* lds_bytes) {
     fa::Elem e;
     if (int st = check_dtype(dtype, &e)) return st;
-    if (!supported_d(d))
+    if (!supported_d(d) && !wide_d(d))
         return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel", (long long)d);
+    if (wide_d(d)) {  // the d-tiled kernels: 64 query rows; K / V chunks of at most 128 columns
+        if (bq) *bq = fa::dtiled_rows_per_block();
+        if (bk) *bk = keys_per_tile(e, d);
+        if (threads) *threads = fa::kThreads;
+        if (lds_bytes) *lds_bytes = e == fa::Elem::F64 ? (64 + 2 * 16) * 129 * 8 + 4 * 16 * 17 * 8 : fa::dtiled_lds_bytes();
+        return ok();
+    }
     if (bq) *bq = fa::kBQ;
     if (bk) *bk = fa::bk_for((int)d);
     if (threads) *threads = fa::kThreads;
@@ -331,9 +360,12 @@ int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o, int64_t B
                  int64_t d, const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
                  double softmax_scale, int dtype, void* stream) {
     fa::Elem e;
-    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_shape(B, H, L, d, true)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
+    if (wide_d(d) && (q_strides || kv_strides || o_strides))
+        return fail(FA_ERR_UNSUPPORTED, "d=%lld: strided tensors not supported (contiguous [B, H, L, d] only)",
+                    (long long)d);
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
     if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
@@ -344,14 +376,25 @@ int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o, int64_t B
 
 int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
                       int64_t L, int64_t d, int d_tile_qk, int d_tile_v, int dtype, void* stream) {
+    return fa_fwd_v1_tiled_d_scaled(q, k, v, o, B, H, L, d, d_tile_qk, d_tile_v,
+                                    1.0 / std::sqrt((double)(d > 0 ? d : 1)), dtype, stream);
+}
+
+int fa_fwd_v1_tiled_d_scaled(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H,
+                             int64_t L, int64_t d, int d_tile_qk, int d_tile_v, double softmax_scale, int dtype,
+                             void* stream) {
     fa::Elem e;
-    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_shape(B, H, L, d, true)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     if (int st = check_d_tiles(d, d_tile_qk, d_tile_v)) return st;
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
-    if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
-        return hip_fail(he, "fa_fwd_v1_tiled_d launch");
+    if (int st = apply_scale(a, softmax_scale)) return st;
+    // d <= 256: one tile holds a whole row -- the fused kernel (its QK^T accumulates 32-column
+    // k-steps, its O^T stays in VGPRs); d = 384 / 512: the d-tiled kernels, tiles honoured
+    const hipError_t he = wide_d(d) ? launch_wide(e, (int)d, a, d_tile_qk, d_tile_v, (hipStream_t)stream)
+                                    : launch_final(e, (int)d, a, (hipStream_t)stream);
+    if (he) return hip_fail(he, "fa_fwd_v1_tiled_d launch");
     return ok();
 }
 
@@ -365,7 +408,7 @@ int fa_fwd_v2_workspace_size_ex(int64_t B, int64_t H, int64_t L, int64_t d, int 
                                 int blocks_per_workgroup, int dtype, int partial_dtype, size_t* bytes,
                                 int* num_splits) {
     fa::Elem e, pe;
-    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_shape(B, H, L, d, true)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (!bytes) return fail(FA_ERR_INVALID_ARG, "bytes is NULL");
@@ -380,7 +423,7 @@ int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tile
                          int blocks_per_workgroup, int dtype, int* key_blocks, int* blocks_per_wg_out,
                          int* partials_per_tile) {
     fa::Elem e;
-    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_shape(B, H, L, d, true)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     SplitPlan p;
     if (int st = plan_splits(B * H, L, d, kv_tiles_per_block, blocks_per_workgroup, e, &p)) return st;
@@ -412,11 +455,14 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
                  void* workspace, size_t workspace_bytes, const int64_t* q_strides, const int64_t* kv_strides,
                  const int64_t* o_strides, double softmax_scale, int dtype, int partial_dtype, void* stream) {
     fa::Elem e, pe;
-    if (int st = check_shape(B, H, L, d)) return st;
+    if (int st = check_shape(B, H, L, d, true)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
     if (int st = check_partial_dtype(partial_dtype, dtype, &pe)) return st;
     if (int st = check_ptrs(q, k, v, o)) return st;
     if (int st = check_d_tiles(d, d_tile_qk, d_tile_v)) return st;
+    if (wide_d(d) && (q_strides || kv_strides || o_strides))
+        return fail(FA_ERR_UNSUPPORTED, "d=%lld: strided tensors not supported (contiguous [B, H, L, d] only)",
+                    (long long)d);
     const int64_t BH = B * H;
     // one plan for the workspace check, the grid and the split length
     SplitPlan sp;
@@ -433,8 +479,9 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     if (int st = apply_scale(a, softmax_scale)) return st;
     if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
     if (ns == 1) {  // one partial workgroup per query tile: nothing to combine
-        if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
-            return hip_fail(he, "fa_fwd_v2 launch");
+        const hipError_t he = wide_d(d) ? launch_wide(e, (int)d, a, d_tile_qk, d_tile_v, (hipStream_t)stream)
+                                        : launch_final(e, (int)d, a, (hipStream_t)stream);
+        if (he) return hip_fail(he, "fa_fwd_v2 launch");
         return ok();
     }
     const V2Layout w = v2_layout(BH, L, d, ns, pe);

@@ -147,6 +147,126 @@ __global__ __launch_bounds__(256, 1) void fa_fwd64_kernel(FwdArgs a) {
     }
 }
 
+// fp64 d-tiled forward for d = 384 / 512 (the head dims past one tile; the reference's tiled-d
+// kernel, flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:230-309, in its USE_FP64 build):
+// per 16-key tile, S = Q K^T accumulated over d_tile_qk-wide column chunks of Q and K staged in
+// LDS -- Q's chunk re-read for every KV tile, as the reference does (:159-164) -- then the
+// online softmax, then O += P V over d_tile_v-wide column chunks of V; O stays in registers
+// (d/4 doubles per lane).  Chunks: the effective tiles of FwdArgs (32, 64 or 128 columns).
+constexpr int kDt64Chunk = 128;  // columns per LDS chunk at most
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void fa_fwd64_dt_kernel(FwdArgs a) {
+    constexpr int LD = kDt64Chunk + 1;  // padded LDS row (doubles)
+    constexpr int NDB = D / 16;
+    __shared__ double qs[kBQ64 * LD];
+    __shared__ double ks[kBK64 * LD];
+    __shared__ double vs[kBK64 * LD];
+    __shared__ double ps[4][16 * 17];
+
+    const int qt = blockIdx.x % a.nqt;
+    const int64_t bh = blockIdx.x / a.nqt;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int g = lane >> 4, j16 = lane & 15;
+    const int nkv = (int)a.Lk;
+    const int dq = a.d_tile_qk, dv = a.d_tile_v, nqc = D / dq, bpc = dv / 16;
+    const double* Q = (const double*)a.q + bh * a.Lq * D;
+    const double* K = (const double*)a.k + bh * a.Lk * D;
+    const double* V = (const double*)a.v + bh * a.Lk * D;
+    const double c = a.scale_log2_64;
+    const int64_t qrow0 = (int64_t)qt * kBQ64;
+    const int64_t row0 = qrow0 + wid * 16;
+
+    f64x4 o[NDB];
+#pragma unroll
+    for (int nb = 0; nb < NDB; ++nb) o[nb] = f64x4{0, 0, 0, 0};
+    double m[4], l[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = -INFINITY;
+        l[r] = 0.0;
+    }
+    const int ntiles = (nkv + kBK64 - 1) / kBK64;
+    for (int t = 0; t < ntiles; ++t) {
+        // S = sum over the K chunks of Q_c K_c^T
+        f64x4 sacc = {0, 0, 0, 0};
+        for (int cq = 0; cq < nqc; ++cq) {
+            __syncthreads();  // previous chunk's reads done
+            for (int e = tid; e < kBQ64 * dq; e += 256) {
+                const int row = e / dq, col = e % dq;
+                qs[row * LD + col] = qrow0 + row < a.Lq ? Q[(qrow0 + row) * D + cq * dq + col] : 0.0;
+            }
+            for (int e = tid; e < kBK64 * dq; e += 256) {
+                const int row = e / dq, col = e % dq;
+                ks[row * LD + col] = t * kBK64 + row < nkv ? K[(int64_t)(t * kBK64 + row) * D + cq * dq + col] : 0.0;
+            }
+            __syncthreads();
+            for (int s4 = 0; s4 < dq / 4; ++s4)
+                sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(qs[(wid * 16 + j16) * LD + 4 * s4 + g],
+                                                            ks[j16 * LD + 4 * s4 + g], sacc, 0, 0, 0);
+        }
+        const bool key_ok = t * kBK64 + j16 < nkv;
+        double p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double s2 = key_ok ? sacc[r] * c : -INFINITY;
+            const double m_new = fmax(m[r], row16_max(s2));
+            const double alpha = exp2(m[r] - m_new);
+            p[r] = exp2(s2 - m_new);
+            l[r] = l[r] * alpha + row16_sum(p[r]);
+            m[r] = m_new;
+#pragma unroll
+            for (int nb = 0; nb < NDB; ++nb) o[nb][r] *= alpha;
+        }
+        double* pw = ps[wid];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[(g + 4 * r) * 17 + j16] = p[r];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double pa[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pa[u] = pw[j16 * 17 + 4 * u + g];
+        // O += P V over the V chunks (column blocks in order; a new chunk every bpc blocks)
+#pragma unroll
+        for (int nb = 0; nb < NDB; ++nb) {
+            if (nb % bpc == 0) {
+                __syncthreads();
+                const int cv = nb / bpc;
+                for (int e = tid; e < kBK64 * dv; e += 256) {
+                    const int row = e / dv, col = e % dv;
+                    vs[row * LD + col] =
+                        t * kBK64 + row < nkv ? V[(int64_t)(t * kBK64 + row) * D + cv * dv + col] : 0.0;
+                }
+                __syncthreads();
+            }
+            const int nl = nb % bpc;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                o[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[u], vs[(4 * u + g) * LD + 16 * nl + j16], o[nb], 0, 0,
+                                                             0);
+        }
+        __builtin_amdgcn_wave_barrier();  // ps is rewritten next tile
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t q_row = row0 + g + 4 * r;
+        if (q_row >= a.Lq) continue;
+        const double inv = 1.0 / l[r];
+        double* Oh = (double*)a.o + (bh * a.Lq + q_row) * D;
+#pragma unroll
+        for (int nb = 0; nb < NDB; ++nb) Oh[16 * nb + j16] = o[nb][r] * inv;
+    }
+}
+
+hipError_t launch_fwd64_dtiled(int d, const FwdArgs& a, hipStream_t s) {
+    const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
+    if (d == 384) hipLaunchKernelGGL((fa_fwd64_dt_kernel<384>), grid, dim3(256), 0, s, a);
+    else if (d == 512) hipLaunchKernelGGL((fa_fwd64_dt_kernel<512>), grid, dim3(256), 0, s, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // O = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M), one thread per output element.
 template <int D>
 __global__ __launch_bounds__(256) void fa_combine64_kernel(CombineArgs a) {

@@ -1,0 +1,282 @@
+// fa_fwd_dtiled.hip -- the d-tiled FA-v1 forward for head dims past one LDS tile (d = 384, 512),
+// bf16 / fp16 storage, fp32 accumulate, on v_mfma_f32_16x16x32.
+//   <- flash_attention_kernel (tiled-d)   flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:230
+//   <- flash_attention_kernel_opt         flash_attention_v1_tiled_d/CUDA/flash_attention_v1_opt.h:366
+//   (semantics: flash_attention_v1_tiled_d/numpy_basic.py:13-151)
+//
+// The reference's tiled-d variant exists so that d can exceed what one tile holds: S = Q K^T is
+// accumulated over d_tile_qk-wide column chunks of K (mat_mul_chunk_accumulate, :57), P V over
+// d_tile_v-wide column chunks of V (accumulate_output_chunk, :105), and O_acc lives in registers
+// for all d columns (:270-272).  Here the same: per 64-key tile, the K tile streams through LDS
+// in [64 keys][d_tile_qk] chunks, the V tile in [64 keys][d_tile_v] chunks, and O^T stays in
+// VGPRs (d/4 registers per lane: 16 query rows per wave, so that d = 512 fits).
+//
+// Tiles are honoured at the MFMA's granularity: a chunk is 32, 64 or 128 columns (the
+// requested d_tile rounded down to one of them, at least 32 -- a QK^T k-step is 32 columns, a
+// P.V output block 16; 32 | 384 and 512), set by the C ABI (fa_capi.cpp dtile_eff) in
+// FwdArgs::d_tile_qk / d_tile_v.  The chunking changes the schedule, not the sums: QK^T
+// accumulates the same 32-column k-steps in the same order whatever the chunk, so outputs are
+// bitwise equal across tile choices (tests/test_gpu.py::test_tiled_d_wide).
+//
+// Geometry (differs from the d <= 256 kernels, whose O^T block per wave is 32 x d):
+//   * workgroup = 4 waves x 16 query rows = 64 rows; the 16 queries of a wave are the B (N)
+//     side of S^T = K . Q^T on v_mfma_f32_16x16x32 (16 keys x 16 queries per MFMA, 4 per tile);
+//   * Q^T fragments in registers for the whole loop (d/32 x 4 VGPRs: 64 at d = 512);
+//   * a query's 64 scores of a tile sit in 4 lanes (n, n+16, n+32, n+48): row max by two
+//     permlane swaps, row sums by a 16x16x32 MFMA with A = ones (as fa_fwd16_kernel.hpp);
+//   * LDS: a 3-slot ring of 16 KiB chunk images (the swizzled 8-row x 32-column subtile image of
+//     fa_device.hpp, row = 2 * chunk bytes), filled by LDS-DMA two chunks ahead of use: the
+//     chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one raw barrier per chunk, the DMA of
+//     chunk i+2 issued right after the barrier that retires chunk i-1's slot;
+//   * registers: d = 384 fits 256 (two workgroups per CU), d = 512 takes 1 wave per SIMD.
+#include "fa_device.hpp"
+
+namespace fa {
+
+constexpr int kDtWaves = 4;
+constexpr int kDtRows = 16 * kDtWaves;  // query rows per workgroup
+constexpr int kDtBK = 64;               // keys per tile
+constexpr int kDtMaxChunk = 128;        // columns per LDS chunk at most
+constexpr int kDtSlotB = kDtBK * kDtMaxChunk * 2;
+constexpr int kDtSlots = 3;
+
+int dtiled_rows_per_block() { return kDtRows; }
+int dtiled_lds_bytes() { return kDtSlots * kDtSlotB; }
+
+// s_waitcnt vmcnt(n) for the DMA pieces a wave may leave in flight (n in {0, 1, 2, 4})
+__device__ __forceinline__ void wait_vm(int n) {
+    if (n >= 4)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n == 2)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n == 1)
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArgs a) {
+    using M = Mma<T>;
+    using v8 = typename M::v8;
+    static_assert(D % 128 == 0 && D > 256 && D <= 512, "d-tiled kernel: d = 384 or 512");
+    constexpr int NKS = D / 32;  // QK^T k-steps
+    constexpr int NDB = D / 16;  // O^T column blocks
+    constexpr int NKB = 4;       // 16-key blocks per tile
+    constexpr int ROWD = 2 * D;  // bytes per global row
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int qt = w % a.nqt;
+    const int64_t bh = w / a.nqt;  // final mode: one split
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n16 = lane & 15, g = lane >> 4;
+    const int nkv = (int)a.Lk;
+    const int ntiles = (nkv + kDtBK - 1) / kDtBK;
+
+    // chunk geometry (effective tiles: 32, 64 or 128 columns, dividing D)
+    const int dq = a.d_tile_qk, dv = a.d_tile_v;
+    const int nqc = D / dq, nvc = D / dv, per_tile = nqc + nvc;
+    const int kpc = dq / 32;          // QK^T k-steps per K chunk
+    const int bpc = dv / 16;          // O^T column blocks per V chunk
+    const int rowq = 2 * dq, rowv = 2 * dv;  // LDS image row bytes
+    const int total = ntiles * per_tile;
+
+    // Q^T fragments (B operand): lane (g, n) holds Q[16*wid + n][32*ks + 8*pg .. +7], the
+    // 8-column chunk permuted over the lane groups as in fa_fwd16_kernel.hpp (A and B agree)
+    const int pg = (0x2130 >> (4 * g)) & 3;
+    const int64_t q_tile0 = (int64_t)qt * kDtRows;
+    const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D + q_tile0 * D;
+    const int64_t q_rows = a.Lq - q_tile0 < kDtRows ? a.Lq - q_tile0 : kDtRows;
+    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, q_rows * ROWD);
+    v8 qf[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+        qf[ks] = __builtin_bit_cast(
+            v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, (wid * 16 + n16) * ROWD + ks * 64 + pg * 16, 0, 0));
+
+    const char* const kbase = (const char*)a.k + bh * a.Lk * ROWD;
+    const char* const vbase = (const char*)a.v + bh * a.Lk * ROWD;
+
+    // LDS-DMA source offsets of this lane's pieces of a chunk image: destination byte b of the
+    // image (rows of `rowb` bytes, swizzled subtiles) <- source row / 16-byte chunk
+    auto src_off = [&](int piece, int rowb) {
+        const int b = piece * 1024 + lane * 16;
+        const int rg = b / (8 * rowb), rem = b % (8 * rowb);
+        const int row = 8 * rg + (rem % 512) / 64;
+        const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
+        return row * ROWD + ch * 16;
+    };
+    const int kpw = dq / 32, vpw = dv / 32;  // pieces per wave of a K / V chunk (1, 2 or 4)
+    int ksrc[4], vsrc[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        ksrc[p] = p < kpw ? src_off(wid * kpw + p, rowq) : 0;
+        vsrc[p] = p < vpw ? src_off(wid * vpw + p, rowv) : 0;
+    }
+    auto pieces = [&](int gi) { return gi >= total ? 0 : (gi % per_tile < nqc ? kpw : vpw); };
+    auto dma_chunk = [&](int gi) {
+        const int t = gi / per_tile, i = gi % per_tile;
+        const bool isk = i < nqc;
+        const int c = isk ? i : i - nqc, dt = isk ? dq : dv;
+        const int valid = nkv - t * kDtBK < kDtBK ? nkv - t * kDtBK : kDtBK;
+        // rows past the last key read zeros (the range ends at the last valid row's chunk)
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc32(
+            (isk ? kbase : vbase) + (int64_t)t * kDtBK * ROWD + c * 2 * dt, (valid - 1) * ROWD + 2 * dt);
+        char* const slot = smem + (gi % kDtSlots) * kDtSlotB;
+        const int pw = isk ? kpw : vpw;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+            if (p < pw) dma16(rs, slot + (wid * pw + p) * 1024, isk ? ksrc[p] : vsrc[p], 0);
+    };
+    // chunk gi becomes readable: its pieces landed (chunk gi+1 may stay in flight), every wave
+    // done with chunk gi-1 (whose slot the DMA of chunk gi+2 then refills)
+    auto advance = [&](int gi) {
+        wait_vm(pieces(gi + 1));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (gi + 2 < total) dma_chunk(gi + 2);
+        return smem + (gi % kDtSlots) * kDtSlotB;
+    };
+
+    // LDS read geometry (fa_fwd16_kernel.hpp): K rows read in the order rho(n), V^T by
+    // transposed reads of the 4 keys at rows R0(g) + (n >> 2) (+16)
+    const int rho = 8 * ((n16 >> 2) & 1) + 4 * (n16 >> 3) + (n16 & 3);
+    const unsigned kl = (rho >> 3) * (8 * rowq) + 64 * (rho & 7) + 16 * (pg ^ ((rho >> 2) & 3));
+    const int r0 = 8 * (g & 1) + 4 * (g >> 1) + (n16 >> 2);
+    const int sw = (r0 >> 2) & 3, c0 = (n16 >> 1) & 1;
+    const unsigned vrow = (r0 >> 3) * (8 * rowv) + 64 * (r0 & 7) + 8 * (n16 & 1);
+    const unsigned vl_e = vrow + 16 * (c0 ^ sw), vl_o = vrow + 16 * ((2 + c0) ^ sw);
+    const int R0 = 8 * (g & 1) + 4 * (g >> 1);  // this lane's first key of each 16-key block
+
+    f32x4 o[NDB];
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) o[db] = f32x4{};
+    f32x4 rs = f32x4{};
+    float m = -INFINITY;
+    v8 ones;
+    {
+        constexpr unsigned kOne = std::is_same_v<T, __bf16> ? 0x3F80u : 0x3C00u;
+        ones = __builtin_bit_cast(v8, u32x4{kOne | (kOne << 16), kOne | (kOne << 16), kOne | (kOne << 16),
+                                            kOne | (kOne << 16)});
+    }
+    const float c = a.scale_log2;
+
+    dma_chunk(0);
+    if (total > 1) dma_chunk(1);
+    int gi = 0;
+    const char* slot = smem;
+    for (int t = 0; t < ntiles; ++t) {
+        // ---- S^T = K Q^T over the d_tile_qk chunks of K
+        f32x4 s[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) s[kb] = f32x4{};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            if (ks % kpc == 0) slot = advance(gi++);
+            const unsigned base = (unsigned)(size_t)slot + kl + (ks % kpc) * 512;
+            u32x4 kf[NKB];
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+                asm volatile("ds_read_b128 %0, %1" : "=v"(kf[kb]) : "v"(base + kb * 16 * rowq) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3])::"memory");
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) s[kb] = M::mma16(__builtin_bit_cast(v8, kf[kb]), qf[ks], s[kb]);
+        }
+        // keys past the end (last tile only): score -inf
+        if (nkv - t * kDtBK < kDtBK) {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (t * kDtBK + 16 * kb + R0 + i >= nkv) s[kb][i] = -INFINITY;
+        }
+        // ---- online softmax (base 2): row max over the 4 lanes of a query, rescale, P
+        float mx = fmax_nc(fmax_nc(s[0][0], s[0][1]), fmax_nc(s[0][2], s[0][3]));
+#pragma unroll
+        for (int kb = 1; kb < NKB; ++kb)
+            mx = fmax_nc(mx, fmax_nc(fmax_nc(s[kb][0], s[kb][1]), fmax_nc(s[kb][2], s[kb][3])));
+        {
+            auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+            const float y = fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
+            auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+            mx = fmax_nc(__uint_as_float(q[0]), __uint_as_float(q[1]));
+        }
+        const float m_new = fmaxf(m, mx * c);
+        if (__builtin_amdgcn_ballot_w64(m_new > m)) {
+            const float alpha = __builtin_amdgcn_exp2f(m - m_new);  // 0 on the first tile
+            rs *= alpha;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+            m = m_new;
+        }
+        u32x4 pbu[2];  // P^T fragments of the two 32-key k-steps (k-order as fa_fwd16_kernel)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kb = 2 * kk + (j >> 1), i = 2 * (j & 1);
+                pbu[kk][j] = pack2<T>(__builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][i], c, -m)),
+                                      __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][i + 1], c, -m)));
+            }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) rs = M::mma16(ones, __builtin_bit_cast(v8, pbu[kk]), rs);
+
+        // ---- O^T += V^T P^T over the d_tile_v chunks of V
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+            if (db % bpc == 0) slot = advance(gi++);
+            const unsigned vb = (unsigned)(size_t)slot + ((db & 1) ? vl_o : vl_e) + 512 * ((db % bpc) >> 1);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                u32x2 v0, v1;
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(vb + kk * 32 * rowv) : "memory");
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(vb + kk * 32 * rowv + 16 * rowv) : "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v0), "+v"(v1)::"memory");
+                const u32x4 vv = {v0[0], v0[1], v1[0], v1[1]};
+                o[db] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[kk]), o[db]);
+            }
+        }
+    }
+
+    // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query n]; dv blocks 2e and 2e+1 are
+    // paired by v_permlane16_swap into one 16-byte store per lane (fa_fwd16_kernel.hpp)
+    const int64_t q_row = q_tile0 + wid * 16 + n16;
+    if (q_row < a.Lq) {
+        const float inv = 1.f / rs[0];
+        unsigned short* const Oh = (unsigned short*)a.o + (bh * a.Lq + q_row) * D;
+#pragma unroll
+        for (int e = 0; e < NDB / 2; ++e) {
+            const unsigned x0 = pack2<T>(o[2 * e][0] * inv, o[2 * e][1] * inv);
+            const unsigned x1 = pack2<T>(o[2 * e][2] * inv, o[2 * e][3] * inv);
+            const unsigned y0 = pack2<T>(o[2 * e + 1][0] * inv, o[2 * e + 1][1] * inv);
+            const unsigned y1 = pack2<T>(o[2 * e + 1][2] * inv, o[2 * e + 1][3] * inv);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+            const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
+            *(u32x4*)(Oh + 32 * e + 16 * (g & 1) + 8 * (g >> 1)) = u;
+        }
+    }
+}
+
+hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s) {
+    const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
+    const int lds = dtiled_lds_bytes();
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kDtWaves * 64), lds, s, a);
+        return hipGetLastError();
+    };
+    if (t == Elem::BF16) {
+        if (d == 384) return go(fa_fwd_dt_kernel<__bf16, 384>);
+        if (d == 512) return go(fa_fwd_dt_kernel<__bf16, 512>);
+    } else if (t == Elem::F16) {
+        if (d == 384) return go(fa_fwd_dt_kernel<_Float16, 384>);
+        if (d == 512) return go(fa_fwd_dt_kernel<_Float16, 512>);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace fa

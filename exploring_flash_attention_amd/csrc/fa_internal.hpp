@@ -73,6 +73,8 @@ struct FwdArgs {
     int strided;
     int64_t H;
     int64_t q_stride[3], k_stride[3], o_stride[3];
+    // d-tiled kernels (d = 384 / 512): effective column chunks of K and V (32, 64 or 128)
+    int d_tile_qk, d_tile_v;
 };
 
 // Kernel modes: one workgroup per (query tile, split, b*h) in all three.
@@ -102,5 +104,11 @@ hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s);
 int fwd64_rows_per_block();
 int fwd64_keys_per_tile();
+// d-tiled forward for d = 384 / 512 (fa_fwd_dtiled.hip; fp64: fa_fwd64.hip), final mode,
+// contiguous [B, H, L, d]; FwdArgs::nqt counts dtiled_rows_per_block() rows per query tile
+hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s);
+hipError_t launch_fwd64_dtiled(int d, const FwdArgs& a, hipStream_t s);
+int dtiled_rows_per_block();
+int dtiled_lds_bytes();
 
 }  // namespace fa

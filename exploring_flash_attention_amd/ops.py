@@ -43,8 +43,11 @@ def _default_pdtype(dtype, partial_dtype, fused=False):
         return torch.float64
     return PARTIAL_FP16_SCALED if fused else torch.float32
 
-SUPPORTED_HEAD_DIMS = (32, 64, 128, 256)  # head dims with a kernel
-MAX_HEAD_DIM = 256
+SUPPORTED_HEAD_DIMS = (32, 64, 128, 256, 384, 512)  # head dims with a kernel
+# head dims past one LDS tile: the d-tiled kernels (csrc/fa_fwd_dtiled.hip), contiguous tensors,
+# FA-v1 / tiled-d / unsplit v2 only (no split-KV partial kernel, no multi-GPU path)
+WIDE_HEAD_DIMS = (384, 512)
+MAX_HEAD_DIM = 512
 
 
 def kernel_head_dim(d):
@@ -156,6 +159,8 @@ def attention_v1(q, k, v, out=None):
     if q.numel() == 0:  # no rows: nothing to launch (the reference returns an empty O)
         return o
     st = _stride_args(q, k, v, o) if D == d else None
+    if st is not None and D in WIDE_HEAD_DIMS:
+        st = False  # the d-tiled kernels address contiguous tensors only
     if st is False:
         return _via_contiguous(attention_v1, q, k, v, o)
     if D == d:
@@ -180,22 +185,36 @@ def _d_tiles(d, d_tile_qk, d_tile_v):
 
 def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
     """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher
-    (0 < d_tile <= d; default min(32, d))."""
+    (0 < d_tile <= d; default min(32, d)).  d <= 256: one LDS tile holds a whole row and the
+    fused kernel runs (tiles validated); 256 < d <= 512: the d-tiled kernel streams K and V
+    through LDS in d_tile-wide column chunks (rounded down to 32, 64 or 128 columns)."""
     _check_qkv(q, k, v, strided=True)
     B, H, L, d = q.shape
     d_tile_qk, d_tile_v = _d_tiles(d, d_tile_qk, d_tile_v)
-    if q.numel() == 0 or kernel_head_dim(d) != d or not all(t.is_contiguous() for t in (q, k, v)) or (
-            out is not None and not out.is_contiguous()):
-        # padded head dims and strided views run on fa_fwd_v1's paths (the same kernel); the
-        # tile arguments are validated against the true d, as the launcher does
-        # (flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327)
-        for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
-            if not 0 < int(t) <= d:
-                raise _lib.FaArgumentError(1, f"{name}={int(t)} must satisfy 0 < {name} <= d={d}")
-        return attention_v1(q, k, v, out=out)
-    o = _out(out, q)
-    check(lib().fa_fwd_v1_tiled_d(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
-                                  int(d_tile_v), _DTYPES[q.dtype], _stream(q)))
+    # the tile arguments are validated against the true d, as the launcher does
+    # (flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327)
+    for name, t in (("d_tile_qk", d_tile_qk), ("d_tile_v", d_tile_v)):
+        if not 0 < int(t) <= d:
+            raise _lib.FaArgumentError(1, f"{name}={int(t)} must satisfy 0 < {name} <= d={d}")
+    D = kernel_head_dim(d)
+    if D not in WIDE_HEAD_DIMS:
+        if q.numel() == 0 or D != d or not all(t.is_contiguous() for t in (q, k, v)) or (
+                out is not None and not out.is_contiguous()):
+            # padded head dims and strided views run on fa_fwd_v1's paths (the same kernel)
+            return attention_v1(q, k, v, out=out)
+        o = _out(out, q)
+        check(lib().fa_fwd_v1_tiled_d(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+                                      int(d_tile_v), _DTYPES[q.dtype], _stream(q)))
+        return o
+    o = _out(out, q, strided=True)
+    if q.numel() == 0:
+        return o
+    qc, kc, vc = (_pad_d(t.contiguous(), D) for t in (q, k, v))
+    oc = o if D == d and o.is_contiguous() else torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
+    check(lib().fa_fwd_v1_tiled_d_scaled(_ptr(qc), _ptr(kc), _ptr(vc), _ptr(oc), B, H, L, D, int(d_tile_qk),
+                                         int(d_tile_v), 1.0 / d ** 0.5, _DTYPES[q.dtype], _stream(q)))
+    if oc is not o:
+        o.copy_(oc[..., :d])
     return o
 
 
@@ -262,6 +281,8 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
     if q.numel() == 0:  # no rows: nothing to launch
         return o
     st = _stride_args(q, k, v, o) if D == d else None
+    if st is not None and D in WIDE_HEAD_DIMS:
+        st = False  # the d-tiled kernels address contiguous tensors only
     if st is False:
         return _via_contiguous(attention_v2, q, k, v, o, kv_tiles_per_block=kv_tiles_per_block,
                                d_tile_qk=d_tile_qk, d_tile_v=d_tile_v, partial_dtype=partial_dtype,

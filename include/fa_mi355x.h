@@ -36,8 +36,9 @@
  *     element type is a runtime argument (FA_DTYPE_BF16, FA_DTYPE_FP16 or FA_DTYPE_FP64);
  *   - the reference fixes the head dim at compile time (assert(d == D),
  *     flash_attention_v1/CUDA/flash_attention_v1.h:264); here d is dispatched at run
- *     time to kernels for d in {32, 64, 128, 256}; any other d returns FA_ERR_UNSUPPORTED
- *     (the *_scaled entry points let a caller zero-pad any d <= 256 to the next one);
+ *     time to kernels for d in {32, 64, 128, 256} and, through fa_fwd_v1 / fa_fwd_v1_tiled_d
+ *     and the unsplit fa_fwd_v2, the d-tiled kernels for d in {384, 512}; any other d returns
+ *     FA_ERR_UNSUPPORTED (the *_scaled entry points let a caller zero-pad any d <= 512);
  *   - sizes are int64_t and every offset is 64-bit (the reference overflows int32 in
  *     its workspace index at L=4096, flash_attention_v2/CUDA/flash_attention_v2.h:324).
  */
@@ -73,7 +74,15 @@ typedef enum fa_dtype {
                                 MFMA, fp64 softmax, fp64 partials and lse */
 } fa_dtype_t;
 
-/* Library version, (major << 16) | (minor << 8) | patch. */
+/* ABI version.  Callers built against one minor version must rebuild for another:
+ *   0.2 -- fa_fwd_v2_ex and fa_fwd_v2_split_plan gained the int blocks_per_workgroup argument
+ *          (inserted before workspace / dtype), fa_fwd_v2_workspace_size_ex was added;
+ *   0.3 -- head dims 384 and 512 (the d-tiled kernels: fa_fwd_v1, fa_fwd_v1_tiled_d, and
+ *          fa_fwd_v2 unsplit), fa_fwd_v1_tiled_d_scaled added.
+ * fa_version() returns the library's (major << 16) | (minor << 8) | patch; check it against
+ * these macros at load time. */
+#define FA_MI355X_VERSION_MAJOR 0
+#define FA_MI355X_VERSION_MINOR 3
 int fa_version(void);
 
 /* Thread-local message describing the last non-FA_OK status on this thread. */
@@ -85,7 +94,8 @@ const char* fa_last_error(void);
 int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads,
                        int* lds_bytes);
 
-/* FA-v1 fused forward.  q, k, v, o: [B, H, L, d] contiguous, element type dtype. */
+/* FA-v1 fused forward.  q, k, v, o: [B, H, L, d] contiguous, element type dtype.
+ * d = 384 / 512 run the d-tiled kernel with 128-column tiles (fa_fwd_v1_tiled_d). */
 int fa_fwd_v1(const void* q, const void* k, const void* v, void* o,
               int64_t B, int64_t H, int64_t L, int64_t d,
               int dtype, void* stream);
@@ -112,19 +122,32 @@ int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o,
                  double softmax_scale, int dtype, void* stream);
 /* FA-v1 d-tiled forward.  d_tile_qk / d_tile_v must satisfy 0 < d_tile <= d
  * (the reference's asserts, flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:326-327),
- * otherwise FA_ERR_INVALID_ARG.  The d-chunking of the arithmetic is set by the MFMA
- * shape (QK^T accumulates over 16-column k-steps, PV produces 32-column O blocks held
- * in VGPRs); the tile arguments are validated as the reference does and do not change
- * the result. */
+ * otherwise FA_ERR_INVALID_ARG.  d in {32, 64, 128, 256, 384, 512}.
+ *   d <= 256: one LDS tile holds a whole row, and the fused kernel runs (its QK^T accumulates
+ *   32-column k-steps, its O stays in VGPRs); the tiles are validated and do not change it.
+ *   d = 384 / 512 (the head dims the variant exists for): the d-tiled kernel streams each
+ *   64-key K tile through LDS in [64][d_tile_qk] column chunks and each V tile in
+ *   [64][d_tile_v] chunks, O_acc in VGPRs for all d columns; a tile is honoured at the MFMA's
+ *   granularity -- rounded down to 32, 64 or 128 columns (at least 32).  QK^T sums the same
+ *   k-steps in the same order whatever the tiles, so the output does not depend on them.
+ * FA_DTYPE_FP64 takes the same paths in fp64 (d = 384 / 512: 16-key tiles, Q chunks re-read
+ * per tile as the reference does, :159-164). */
 int fa_fwd_v1_tiled_d(const void* q, const void* k, const void* v, void* o,
                       int64_t B, int64_t H, int64_t L, int64_t d,
                       int d_tile_qk, int d_tile_v,
                       int dtype, void* stream);
+/* fa_fwd_v1_tiled_d with an explicit softmax scale (as fa_fwd_v1_scaled: lets a caller zero-pad
+ * a head dim without its own kernel, e.g. 257..511, to 384 or 512; the tiles are checked
+ * against the d passed here). */
+int fa_fwd_v1_tiled_d_scaled(const void* q, const void* k, const void* v, void* o,
+                             int64_t B, int64_t H, int64_t L, int64_t d,
+                             int d_tile_qk, int d_tile_v, double softmax_scale,
+                             int dtype, void* stream);
 
 /* kv_tiles_per_block value that lets the library choose the split from the device's
- * occupancy: no split when the query tiles fill the GPU, otherwise about two workgroups
- * per resident slot (the reference's README presets, flash_attention_v2/README.md:29-32,
- * made automatic). */
+ * occupancy: no split when the query tiles alone number at least the device's compute units,
+ * otherwise about one workgroup per CU (the reference's README presets,
+ * flash_attention_v2/README.md:29-32, made automatic). */
 #define FA_KV_TILES_AUTO (-1)
 
 /* blocks_per_workgroup value that lets the library group the key blocks of a query tile onto
@@ -149,7 +172,9 @@ int fa_fwd_v2_workspace_size_ex(int64_t B, int64_t H, int64_t L, int64_t d,
  * * bk)) (the reference's partials), *blocks_per_wg_out consecutive blocks per workgroup
  * (combined on chip: the online softmax carried across them), *partials_per_tile partial
  * workgroups per query tile (combined through the workspace).  With blocks_per_workgroup =
- * FA_BLOCKS_PER_WG_AUTO blocks are grouped as long as >= 4 workgroups per resident slot remain;
+ * FA_BLOCKS_PER_WG_AUTO the library cuts the blocks of a query tile into equal groups: none beyond
+ * one when the query tiles alone number at least the device's compute units, otherwise
+ * ceil(CUs / query tiles) groups (about one workgroup per CU; d = 384 / 512: always one group);
  * a positive value fixes the group size (1: one workgroup and one HBM partial per key block, the
  * reference's layout; clamped to the number of blocks).  The plan depends only on the
  * arguments and the device's compute-unit count.  Any output pointer may be NULL. */

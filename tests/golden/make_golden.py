@@ -3,7 +3,7 @@
 Run in the build container only (it needs /root/reference, which does not exist on the
 GPU box; the committed .npz files travel instead):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [wide]
 
 Every fixture stores its inputs, the reference function's output(s) and the reference
 naive_attention output, plus a ``call`` string naming the reference function and
@@ -44,8 +44,26 @@ def _save(name, **arrays):
     print(f"wrote {path} ({os.path.getsize(path)} bytes)")
 
 
+def wide(ref, tdb):
+    """g6: tiled-d at a head dim past one tile (d = 384), the case the reference's tiled-d variant
+    exists for: L=16, ragged d tiles (100 / 96 columns: chunks 100,100,100,84 and 4 x 96); inputs are multiples of 1/16 in [-2, 2) stored as int8 (exact in every
+    float type), computed in fp64."""
+    rng = np.random.default_rng(6)
+    qi, ki, vi = (rng.integers(-32, 32, (16, 384)).astype(np.int8) for _ in range(3))
+    Q, K, V = (x.astype(np.float64) / 16 for x in (qi, ki, vi))
+    outs = {}
+    for (dq, dv) in ((100, 96),):
+        outs[f"O_{dq}_{dv}"] = tdb.flash_attention_tiled_global(Q, K, V, Bq=8, Bk=8, d_tile_qk=dq, d_tile_v=dv)
+    _save("g6_tiled_d_d384.npz", Q16=qi, K16=ki, V16=vi, O_naive=ref.naive_attention(Q, K, V), **outs,
+          call=np.array("flash_attention_v1_tiled_d/numpy_basic.py flash_attention_tiled_global(Q,K,V,Bq=8,Bk=8,"
+                        "d_tile_qk,d_tile_v) with Q = Q16 / 16 etc."))
+
+
 def main():
     ref = _load("common/reference.py", "ref_common")
+    if sys.argv[1:] == ["wide"]:  # only g6 (the others unchanged)
+        wide(ref, _load("flash_attention_v1_tiled_d/numpy_basic.py", "ref_td_basic"))
+        return
     v1b = _load("flash_attention_v1/numpy_basic.py", "ref_v1_basic")
     v1o = _load("flash_attention_v1/numpy_gpu_like_opt2.py", "ref_v1_opt2")
     tdb = _load("flash_attention_v1_tiled_d/numpy_basic.py", "ref_td_basic")
@@ -120,6 +138,7 @@ def main():
                                 for h in range(2)]) for b in range(1)]).astype(np.float32)
         _save(f"g5_driver_d{d}.npz", Q=x[0], K=x[1], V=x[2], O=O,
               call=np.array("common/reference.py naive_attention per (b,h) on driver.cu srand(42) inputs"))
+    wide(ref, tdb)
 
 
 if __name__ == "__main__":

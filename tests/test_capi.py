@@ -39,7 +39,11 @@ def test_exports_are_c_symbols_not_mangled():
 
 
 def test_version_and_geometry():
-    assert L.lib().fa_version() == 0x000100
+    # ABI 0.3 (include/fa_mi355x.h FA_MI355X_VERSION_*): blocks_per_workgroup in 0.2, d = 384 / 512
+    hdr = open(os.path.join(ROOT, "include", "fa_mi355x.h")).read()
+    major = int(re.search(r"#define FA_MI355X_VERSION_MAJOR (\d+)", hdr).group(1))
+    minor = int(re.search(r"#define FA_MI355X_VERSION_MINOR (\d+)", hdr).group(1))
+    assert L.lib().fa_version() == (major << 16) | (minor << 8) == 0x000300
     bq, bk, threads, lds = L.geometry(128)
     assert (bq, bk, threads) == (128, 64, 256)
     assert lds == 2 * 2 * 64 * 128 * 2
@@ -49,6 +53,9 @@ def test_version_and_geometry():
     assert (bq, bk, threads, lds) == (128, 32, 256, 2 * 2 * 32 * 256 * 2)
     with pytest.raises(L.FaArgumentError):
         L.geometry(96)
+    # the d-tiled kernels: 64 query rows, 64-key tiles, a 3-slot ring of 16 KiB chunk images
+    assert L.geometry(512) == (64, 64, 256, 3 * 16384) and L.geometry(384)[:3] == (64, 64, 256)
+    assert L.geometry(384, L.FA_DTYPE_FP64)[:3] == (64, 16, 256)
 
 
 NULL = ctypes.c_void_p(0)
@@ -110,7 +117,8 @@ def test_kernel_head_dim_padding_map():
     from exploring_flash_attention_amd import ops
     assert [ops.kernel_head_dim(d) for d in (1, 16, 32, 33, 48, 64, 80, 96, 128, 129, 200, 256)] == \
         [32, 32, 32, 64, 64, 64, 128, 128, 128, 256, 256, 256]
-    for bad in (0, -4, 257, 512):
+    assert [ops.kernel_head_dim(d) for d in (257, 300, 384, 385, 500, 512)] == [384, 384, 384, 512, 512, 512]
+    for bad in (0, -4, 513, 1024):
         with pytest.raises(ValueError):
             ops.kernel_head_dim(bad)
 
@@ -161,7 +169,8 @@ def test_workspace_size_and_v2_checks():
     # 256 query tiles already occupy every CU: no split (measured: 8 partials there lose 10 %)
     assert lib.fa_fwd_v2_split_plan(1, 2, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
                                     ctypes.byref(p)) == 0 and p.value == 1
-    # 128 query tiles: two partials each; 100 query tiles: 3 (groups of ceil(64/3) = 22 blocks)
+    # 128 query tiles: two partials each; 100 query tiles: ceil(256 / 100) = 3 (its 50 key blocks in
+    # groups of ceil(50 / 3) = 17)
     assert lib.fa_fwd_v2_split_plan(1, 1, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
                                     ctypes.byref(p)) == 0 and (g.value, p.value) == (32, 2)
     assert lib.fa_fwd_v2_split_plan(1, 1, 12800, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),

@@ -619,3 +619,73 @@ def test_scaled_partials_near_bf16_max(gpu):
         o = o.double().cpu().numpy()
         assert np.isfinite(o).all(), name
         assert np.abs(o - ref).max() <= 1e-2 * 2.0 ** 127, name
+
+
+# ----------------------------------------------------------------------------------------
+# head dims past one tile: the d-tiled kernels (csrc/fa_fwd_dtiled.hip, fa_fwd64.hip)
+# ----------------------------------------------------------------------------------------
+
+WIDE_TILES = [(32, 32), (64, 128), (128, 64), (100, 48), (512, 512)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("d", [384, 512])
+@pytest.mark.parametrize("L", [200, 256], ids=["keytail", "notail"])
+def test_tiled_d_wide(gpu, d, dtype, L):
+    """fa_fwd_v1_tiled_d at d = 384 / 512: K and V stream through LDS in d_tile-wide column
+    chunks (flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:137-227), O in VGPRs.  Every
+    tile choice gives the same bits (the same k-steps in the same order), within the gates of
+    the fp64 oracle; fa_fwd_v1 (128-column tiles) and the unsplit v2 agree."""
+    from exploring_flash_attention_amd import ops
+    q, k, v = _inputs(2, 3, L, d, dtype, seed=d + L)
+    ref = _ref(q, k, v)
+    qd, kd, vd = q.cuda(), k.cuda(), v.cuda()
+    outs = []
+    for dq, dv in WIDE_TILES:
+        if dq > d or dv > d:
+            continue
+        outs.append(ops.attention_tiled_d(qd, kd, vd, dq, dv))
+    torch.cuda.synchronize()
+    _gate(outs[0], ref, dtype)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    assert torch.equal(ops.attention_v1(qd, kd, vd), outs[0])
+    assert torch.equal(ops.attention_v2(qd, kd, vd, kv_tiles_per_block=4), outs[0])
+
+
+@pytest.mark.parametrize("d", [384, 512])
+def test_tiled_d_wide_fp64(gpu, d):
+    """The fp64 d-tiled kernel (Q chunks re-read per KV tile, as the reference's kernel) holds
+    1e-12 against the fp64 oracle for every tile choice, with key and query tails."""
+    from exploring_flash_attention_amd import ops
+    q, k, v = _inputs(1, 2, 77, d, torch.float64, seed=d)
+    ref = _ref(q, k, v)
+    qd, kd, vd = q.cuda(), k.cuda(), v.cuda()
+    for dq, dv in WIDE_TILES:
+        o = ops.attention_tiled_d(qd, kd, vd, min(dq, d), min(dv, d))
+        assert np.abs(o.cpu().numpy() - ref).max() <= 1e-12, (dq, dv)
+    assert np.abs(ops.attention_v1(qd, kd, vd).cpu().numpy() - ref).max() <= 1e-12
+
+
+def test_tiled_d_wide_golden_and_padding(gpu):
+    """The reference's own tiled-d output at d = 384 (golden g6, ragged d tiles 100 / 96)
+    through the NumPy surface (fp64 kernels); head dims between the kernels (300, 400) are
+    zero-padded to 384 / 512 with the true d's scale; strided views and the C tile checks."""
+    from exploring_flash_attention_amd import ops, tiled_d
+    g = golden("g6_tiled_d_d384.npz")
+    Q, K, V = (g[n].astype(np.float64) / 16 for n in ("Q16", "K16", "V16"))
+    O = tiled_d.flash_attention_tiled_global(Q, K, V, 8, 8, 100, 96)
+    assert O.dtype == np.float64 and np.abs(O - g["O_100_96"]).max() <= 1e-12
+    for d in (300, 400):
+        q, k, v = _inputs(2, 2, 130, d, torch.bfloat16, seed=d)
+        ref = _ref(q, k, v)
+        _gate(ops.attention_tiled_d(q.cuda(), k.cuda(), v.cuda(), 64, 96), ref, torch.bfloat16)
+        _gate(ops.attention_v1(q.cuda(), k.cuda(), v.cuda()), ref, torch.bfloat16)
+        with pytest.raises(ops._lib.FaArgumentError):
+            ops.attention_tiled_d(q.cuda(), k.cuda(), v.cuda(), d + 1, 32)
+    # a [B, L, H, d] tensor viewed as [B, H, L, d]: copied to contiguous for the d-tiled kernel
+    x = _inputs(2, 130, 3, 384, torch.bfloat16, seed=5)
+    qs, ks, vs = (t.cuda().transpose(1, 2) for t in x)
+    ref = _ref(*(t.cpu().contiguous() for t in (qs, ks, vs)))
+    _gate(ops.attention_tiled_d(qs, ks, vs, 128, 128), ref, torch.bfloat16)
+    _gate(ops.attention_v1(qs, ks, vs), ref, torch.bfloat16)

@@ -244,3 +244,31 @@ def test_replay_catches_a_bad_decode():
     replay(a, allocs, True)  # the real decode: in bounds
     with pytest.raises(AssertionError, match="decoded up to"):
         replay(a, allocs, True, flat_decode=True)
+
+
+@pytest.mark.parametrize("B,H,L,d", [(32, 8, 1024, 512), (2, 3, 200, 384), (1, 1, 1, 512), (1, 2, 77, 384)])
+@pytest.mark.parametrize("dq,dv", [(32, 32), (128, 64), (64, 128)])
+def test_dtiled_kernel_in_bounds(B, H, L, d, dq, dv):
+    """csrc/fa_fwd_dtiled.hip (d = 384 / 512): 64-row query tiles; per 64-key tile the K and V
+    column chunks [64][dt] are DMA'd through descriptors that start at the chunk's first column
+    and end at the last valid key's chunk end."""
+    BH, D, ROWD = B * H, d, 2 * d
+    nqt = -(-L // 64)
+    nblk = nqt * BH
+    w = xcd_remap(np.arange(nblk, dtype=np.int64), nblk)
+    assert np.array_equal(np.sort(w), np.arange(nblk))
+    qt, bh = w % nqt, w // nqt
+    q, k, v, o = (_tensor(n, B, H, L, d) for n in "qkvo")
+    q_tile0 = qt * 64
+    q_rows = np.minimum(L - q_tile0, 64)
+    q.check(2 * (bh * L * D + q_tile0 * D), q_rows * ROWD, "Q descriptor")
+    ntiles = -(-L // 64)
+    for t in range(ntiles):
+        valid = min(64, L - t * 64)
+        for alloc, dt in ((k, dq), (v, dv)):
+            for c in range(D // dt):
+                base = bh * L * ROWD + t * 64 * ROWD + c * 2 * dt
+                alloc.check(base, (valid - 1) * ROWD + 2 * dt, f"chunk t={t} c={c}")
+    rows = q_tile0[:, None] + np.arange(64)[None, :]
+    live = rows < L
+    o.check(np.where(live, 2 * (bh[:, None] * L * D + rows * D), 0), np.where(live, ROWD, 0), "O row store")

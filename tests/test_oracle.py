@@ -159,3 +159,13 @@ def test_half_bfloat_conversions(oracle_lib):
     ref = torch.from_numpy(x).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
     np.testing.assert_array_equal(b, ref)
     _ = ctypes  # keep import used
+
+
+def test_tiled_d_restatement_at_a_wide_head_dim():
+    """g6 (d = 384, ragged d tiles 100 / 96): the reference's own tiled-d output at a head dim
+    past one tile, the case the d-tiled kernels (csrc/fa_fwd_dtiled.hip) serve."""
+    g = golden("g6_tiled_d_d384.npz")
+    Q, K, V = (g[n].astype(np.float64) / 16 for n in ("Q16", "K16", "V16"))
+    O = tiled_d.flash_attention_tiled_global(Q, K, V, 8, 8, 100, 96)
+    np.testing.assert_allclose(O, g["O_100_96"], rtol=0, atol=TIGHT)
+    np.testing.assert_allclose(g["O_naive"], g["O_100_96"], rtol=0, atol=TIGHT)
