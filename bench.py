@@ -289,6 +289,9 @@ def c5_breakdown(torch, ops, fdist, dev, world, rank, barrier):
 EXTRA_SHAPES = (
     # name, B, H, L, d, variant, kv_tiles_per_block, blocks_per_workgroup
     ("c2_fused", 32, 8, 1024, 32, "v1", None, None),
+    # head dims past one tile: the d-tiled kernel (K / V column chunks of d_tile = 128 columns)
+    ("d384_tiled_d", 32, 8, 1024, 384, "tiled_d", None, None),
+    ("d512_tiled_d", 32, 8, 1024, 512, "tiled_d", None, None),
     ("c4_splitkv", 32, 8, 4096, 128, "v2", 4, None),
     ("c4_splitkv_4_blocks_per_wg", 32, 8, 4096, 128, "v2", 4, 4),
     ("c4_splitkv_1_block_per_wg", 32, 8, 4096, 128, "v2", 4, 1),
@@ -312,6 +315,10 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
         if fn == "v1":
             def st():
                 ops.attention_v1(qq, kk, vv)
+        elif fn == "tiled_d":
+            def st():
+                ops.attention_tiled_d(qq, kk, vv, 128, 128)
+            rec.update(d_tile_qk=128, d_tile_v=128, kernel=f"fa_fwd_dt_kernel (d = {d})")
         else:
             if grp == "all":  # every key block of a query tile on one workgroup: no split
                 grp = ops.v2_split_plan(B, H, L, d, kvt, qq.dtype)[0]

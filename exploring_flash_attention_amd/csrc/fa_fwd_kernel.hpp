@@ -123,10 +123,9 @@ __global__ __launch_bounds__(kThreads, kernel_wps(D, MODE, TAIL, STRIDED)) void 
     char* const vring = smem + 2 * TILEB;
 
     const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const int qt = w % a.nqt;
-    const int rest = w / a.nqt;
-    const int split = rest % a.nsplit;
-    const int64_t bh = rest / a.nsplit;
+    int qt, split;
+    int64_t bh;
+    decode_item(a, w, qt, split, bh);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;

@@ -75,7 +75,26 @@ struct FwdArgs {
     int64_t q_stride[3], k_stride[3], o_stride[3];
     // d-tiled kernels (d = 384 / 512): effective column chunks of K and V (32, 64 or 128)
     int d_tile_qk, d_tile_v;
+    // fused split mode: the order of the work items in the (remapped) block index -- 0: query
+    // tile fastest (the 32 tiles of one key block share its K / V in L2), 1: split fastest (the
+    // splits of one query tile run together: Q re-read from L2, partials combined while hot)
+    int split_fastest;
 };
+
+// (query tile, split, b*h) of work item w (after xcd_remap)
+__device__ __forceinline__ void decode_item(const FwdArgs& a, int w, int& qt, int& split, int64_t& bh) {
+    if (a.split_fastest) {
+        split = w % a.nsplit;
+        const int rest = w / a.nsplit;
+        qt = rest % a.nqt;
+        bh = rest / a.nqt;
+    } else {
+        qt = w % a.nqt;
+        const int rest = w / a.nqt;
+        split = rest % a.nsplit;
+        bh = rest / a.nsplit;
+    }
+}
 
 // Kernel modes: one workgroup per (query tile, split, b*h) in all three.
 enum Mode : int {

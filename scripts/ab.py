@@ -26,10 +26,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--acc", action="store_true", help="also report the error against fp32")
     ap.add_argument("--kvtpb", type=int, default=0, help="time fa_fwd_v2 with this kv_tiles_per_block")
+    ap.add_argument("--bpw", type=int, default=0,
+                    help="with --kvtpb: blocks_per_workgroup of fa_fwd_v2_ex (0 = the library's grouping)")
+    ap.add_argument("--shape", default="", help="B,H,L,d instead of --config")
     ap.add_argument("--partial", action="store_true",
                     help="time fa_fwd_partial over all keys (scaled fp16 partials: the C5 per-rank kernel)")
     args = ap.parse_args()
-    B, H, L, d = CFG[args.config]
+    B, H, L, d = tuple(int(x) for x in args.shape.split(",")) if args.shape else CFG[args.config]
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(B, H, L, d, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
     outs = [torch.empty_like(q) for _ in args.libs]
@@ -43,12 +46,18 @@ def main():
                                      [ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
         h.fa_fwd_v2_workspace_size.argtypes = [ctypes.c_int64] * 4 + [ctypes.c_int] * 3 + [
             ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]
+        h.fa_fwd_v2_workspace_size_ex.argtypes = [ctypes.c_int64] * 4 + [ctypes.c_int] * 4 + [
+            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]
+        h.fa_fwd_v2_ex.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_int64] * 4 + [ctypes.c_int] * 4 +
+                                   [ctypes.c_void_p, ctypes.c_size_t] + [ctypes.c_void_p] * 3 +
+                                   [ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
         libs.append(h)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ws = None
     if args.kvtpb:  # FA-v2 split-KV (in-kernel combine), scaled fp16 partials
         nb, ns = ctypes.c_size_t(), ctypes.c_int()
-        assert libs[0].fa_fwd_v2_workspace_size(B, H, L, d, args.kvtpb, 1, 4, ctypes.byref(nb), ctypes.byref(ns)) == 0
+        assert libs[0].fa_fwd_v2_workspace_size_ex(B, H, L, d, args.kvtpb, args.bpw, 1, 4, ctypes.byref(nb),
+                                                   ctypes.byref(ns)) == 0
         ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
         print(f"v2: kv_tiles_per_block {args.kvtpb}, {ns.value} splits, workspace {nb.value / 1e9:.2f} GB")
 
@@ -63,8 +72,9 @@ def main():
                                         part[i][1].data_ptr(), B, H, L, L, d, L, 1, 4, stream)
             outs[i] = part[i][0]
         elif ws is not None:
-            st = libs[i].fa_fwd_v2(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d,
-                                   min(32, d), min(32, d), args.kvtpb, ws.data_ptr(), ws.numel(), 1, 4, stream)
+            st = libs[i].fa_fwd_v2_ex(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d,
+                                      min(32, d), min(32, d), args.kvtpb, args.bpw, ws.data_ptr(), ws.numel(),
+                                      None, None, None, 1.0 / d ** 0.5, 1, 4, stream)
         else:
             st = libs[i].fa_fwd_v1(q.data_ptr(), k.data_ptr(), v.data_ptr(), outs[i].data_ptr(), B, H, L, d, 1, stream)
         assert st == 0, st

@@ -9,4 +9,8 @@ hipError_t launch_fwd64(int, Mode, const FwdArgs&, hipStream_t) { return hipErro
 hipError_t launch_combine64(int, const CombineArgs&, hipStream_t) { return hipErrorInvalidValue; }
 int fwd64_rows_per_block() { return 64; }
 int fwd64_keys_per_tile() { return 16; }
+hipError_t launch_fwd_dtiled(Elem, int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_fwd64_dtiled(int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
+int dtiled_rows_per_block() { return 64; }
+int dtiled_lds_bytes() { return 3 * 16384; }
 }  // namespace fa
