@@ -11,9 +11,12 @@ Reference surfaces mirrored (tyler-utah/exploring_flash_attention):
   ``flash_attention_v1_opt``)
       flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:312, flash_attention_v1_opt.h:448
 
-On gfx950 the QK^T product accumulates over 16-column MFMA k-steps and O_acc is held in
-VGPRs as 32-column blocks for the whole KV loop; the d-tile arguments are validated like
-the reference's (0 < d_tile <= d) and do not change the result.
+The d-tile arguments are validated like the reference's (0 < d_tile <= d).  For d <= 256 one
+LDS tile holds a whole row and the fused kernel runs (its QK^T accumulates 32-column MFMA
+k-steps, O_acc stays in VGPRs), the tiles not changing the result; for 256 < d <= 512 the
+d-tiled kernel (csrc/fa_fwd_dtiled.hip) streams K and V through LDS in d_tile-wide column
+chunks (rounded down to 32, 64 or 128 columns), O_acc in VGPRs for all d columns -- the case
+the reference's variant exists for.
 """
 import numpy as np
 

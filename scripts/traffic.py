@@ -19,16 +19,17 @@ import sys
 def main():
     d, cfg = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else None
-    vals = {}
+    vals, kernels = {}, set()
     for f in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if not re.search(r"fa_fwd(16)?_kernel", r["Kernel_Name"]):
+            if not re.search(r"fa_fwd(16|_dt)?_kernel", r["Kernel_Name"]):
                 continue
+            kernels.add(r["Kernel_Name"].split("(")[0])
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     mean = {k: sum(v) / len(v) for k, v in vals.items()}
     fetch = mean.get("FETCH_SIZE")
     write = mean.get("WRITE_SIZE")
-    rec = {"counters_mean": mean}
+    rec = {"counters_mean": mean, "kernels": sorted(kernels)}
     if fetch is not None and write is not None:
         rec["read_bytes_per_launch"] = 2 * fetch * 1024
         rec["write_bytes_per_launch"] = write * 1024
