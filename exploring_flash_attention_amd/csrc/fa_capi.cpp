@@ -299,7 +299,8 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
 }
 
 // Work order of the fused split launch (FwdArgs::split_fastest): split fastest when the whole
-// grid is resident at once (at most two workgroups per CU), query tile fastest otherwise.
+// grid is resident at once (at most two workgroups per CU) and a query tile has at least 4
+// partials, query tile fastest otherwise.
 // Measured (round 4, A/B in one process, profiles/r04/ab_split_order.log; outputs bitwise
 // equal): B1 H2 L4096 (4 partials, 256 workgroups) 30.9 -> 28.9 us; B1 H1 L16384 (2 partials,
 // 256) 132.2 -> 131.5 us; but B2 H2 L16384 (4 partials, 2048) -1.6 %, C4 with 4 partials per
@@ -309,9 +310,11 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
 #ifndef FA_SPLIT_ORDER_RULE
 #define FA_SPLIT_ORDER_RULE 2  // 0: query tile fastest always; 1: split fastest always; 2: the rule
 #endif
-int split_fastest(int64_t nblk) {
+int split_fastest(int64_t nblk, int ns) {
     if (FA_SPLIT_ORDER_RULE != 2) return FA_SPLIT_ORDER_RULE == 1;
-    return nblk <= 2 * (int64_t)device_cus();
+    // (B1 H1 L16384, 2 partials: equal time either way, but split fastest puts both halves of
+    // the keys on every XCD -- 93 MB of L2 egress per launch against 64 MB (profiles/r04))
+    return ns >= 4 && nblk <= 2 * (int64_t)device_cus();
 }
 
 // workspace bytes for a plan (the grid bound checked too)
@@ -519,7 +522,7 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     a.o = workspace;
     a.lse = (float*)((char*)workspace + w.lse_off);
     a.esc = (float*)((char*)workspace + w.esc_off);
-    a.split_fastest = split_fastest((int64_t)a.nqt * ns * BH);
+    a.split_fastest = split_fastest((int64_t)a.nqt * ns * BH, ns);
     a.counters = (unsigned*)((char*)workspace + w.cnt_off);
     a.o_final = o;
     // the kernel leaves every counter at zero; clearing them here makes a call that follows

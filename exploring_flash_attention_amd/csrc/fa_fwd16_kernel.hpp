@@ -56,9 +56,13 @@ template <typename X> struct TypeTag { using type = X; };
 // MODE: kFinal (O), kPartial (normalised partial O + lse in row layout, fa_combine.hip reads
 // them) or kFused (partials in fragment order, combined by the last workgroup of each query
 // tile), as fa_fwd_kernel.hpp; every split a multiple of 64 keys and non-empty.
-// QSTR: q is a strided view whose rows are contiguous (row stride d) -- the row ranges of the
-// multi-GPU partial path (fa_fwd_partial_ex); its heads are addressed through q_stride[0..1].
-template <typename T, typename PT, int D, int MODE, bool QSTR = false>
+// STR: q, k / v and o are [B, H, L, d] views addressed through their {batch, head, row}
+// element strides (FwdArgs q_stride / k_stride / o_stride; d contiguous, rows 16-byte aligned),
+// e.g. [B, L, H, d] tensors transposed, or the q row ranges of the multi-GPU partial path
+// (fa_fwd_partial_ex).  Only the global addressing changes -- the DMA source offsets and tile
+// descriptors take the row stride -- so a view gives the contiguous launch's bits.  (Partial
+// mode writes its own row layout; o_stride is not used there.)
+template <typename T, typename PT, int D, int MODE, bool STR = false>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
@@ -96,12 +100,22 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     const int ntiles = (int)((kv_end - kv_begin) / kBK);
 
     const int64_t q_tile0 = (int64_t)qt * kBQ;
-    const int64_t q_head = QSTR ? (bh / a.H) * a.q_stride[0] + (bh % a.H) * a.q_stride[1] : bh * a.Lq * D;
-    const unsigned short* Qh = (const unsigned short*)a.q + q_head + q_tile0 * D;
+    // row strides (bytes) and head bases (elements); contiguous launches fold them to constants
+    const int qrb = STR ? (int)(a.q_stride[2] * 2) : ROWB;
+    const int krb = STR ? (int)(a.k_stride[2] * 2) : ROWB;
+    const int64_t hb = STR ? bh / a.H : 0, hh = STR ? bh - hb * a.H : 0;
+    const int64_t q_head = STR ? hb * a.q_stride[0] + hh * a.q_stride[1] : bh * a.Lq * D;
+    const int64_t k_head = STR ? hb * a.k_stride[0] + hh * a.k_stride[1] : bh * a.Lk * D;
+    const int64_t o_head = STR ? hb * a.o_stride[0] + hh * a.o_stride[1] : bh * a.Lq * D;
+    const int64_t orow = STR ? a.o_stride[2] : D;
+    const unsigned short* Qh = (const unsigned short*)a.q + q_head + q_tile0 * (qrb / 2);
     const int64_t q_rows = a.Lq - q_tile0 < kBQ ? a.Lq - q_tile0 : kBQ;
-    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, q_rows * ROWB);
-    const unsigned short* const kbase = (const unsigned short*)a.k + (bh * a.Lk + kv_begin) * D;
-    const unsigned short* const vbase = (const unsigned short*)a.v + (bh * a.Lk + kv_begin) * D;
+    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, (q_rows - 1) * qrb + ROWB);
+    const unsigned short* const kbase = (const unsigned short*)a.k + k_head + kv_begin * (krb / 2);
+    const unsigned short* const vbase = (const unsigned short*)a.v + k_head + kv_begin * (krb / 2);
+    // one K / V tile in global memory: its stride and the bytes its descriptor covers
+    const int64_t tstride = STR ? (int64_t)kBK * krb : (int64_t)TILEB;
+    const int tbytes = STR ? (kBK - 1) * krb + ROWB : TILEB;
 
     // The 32 dims of a QK^T k-step are split over the lane groups g as 8-dim chunk pg(g) =
     // (0, 3, 1, 2)[g] (A and B agree, so the sum is the same): ds_read_b128 serves a wave in the
@@ -115,7 +129,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
             qf[qb][ks] = __builtin_bit_cast(
-                v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, (wid * 32 + 16 * qb + n16) * ROWB + ks * 64 + pg * 16, 0, 0));
+                v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, (wid * 32 + 16 * qb + n16) * qrb + ks * 64 + pg * 16, 0, 0));
 
     // LDS-DMA of a tile: 16 pieces of 1 KiB, 4 per wave, the swizzled image (lds_off) produced
     // by giving each lane the SOURCE chunk that lands at its destination (fa_fwd_kernel.hpp)
@@ -127,10 +141,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         const int rg = b / (8 * ROWB), rem = b % (8 * ROWB);
         const int row = 8 * rg + (rem % 512) / 64;
         const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
-        dma_src[i] = row * ROWB + ch * 16;
+        dma_src[i] = row * krb + ch * 16;
     }
     auto dma_tile = [&](const unsigned short* base, char* slot, int t) {
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc32((const char*)base + (int64_t)t * TILEB, t < ntiles ? TILEB : 0);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc32((const char*)base + t * tstride, t < ntiles ? tbytes : 0);
 #pragma unroll
         for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], 0);
     };
@@ -255,8 +269,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         }
         const float nm0 = -m[0], nm1 = -m[1];
         const __amdgpu_buffer_rsrc_t krs =
-            make_rsrc32((const char*)kbase + (int64_t)(t + 2) * TILEB, DMAK && t + 2 < ntiles ? TILEB : 0);
-        const __amdgpu_buffer_rsrc_t vrs = make_rsrc32((const char*)vbase + (int64_t)(t + 1) * TILEB, TILEB);
+            make_rsrc32((const char*)kbase + (t + 2) * tstride, DMAK && t + 2 < ntiles ? tbytes : 0);
+        const __amdgpu_buffer_rsrc_t vrs = make_rsrc32((const char*)vbase + (t + 1) * tstride, tbytes);
         char* const kdst = kring + P * TILEB + wid * DPW * 1024;
         char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
 
@@ -443,7 +457,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
 #pragma unroll
         for (int qb = 0; qb < NQB; ++qb) {
             const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
-            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o + (bh * a.Lq + q_row) * D, ov[qb], inv[qb]);
+            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o + o_head + q_row * orow, ov[qb], inv[qb]);
         }
     } else if constexpr (MODE == kPartial) {
 #pragma unroll
@@ -569,7 +583,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
                 inv_w = 1.f;
             }
             const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
-            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o_final + (bh * a.Lq + q_row) * D, acc, inv_w);
+            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o_final + o_head + q_row * orow, acc, inv_w);
         }
     }
 }

@@ -2,7 +2,9 @@
 // tensors: [B, H, L, d] views with arbitrary (batch, head, row) element strides and a
 // contiguous d, e.g. the [B, L, H, d] layout most frameworks keep, with no copy.  Final mode
 // (FA-v1 fused / d-tiled), the fused split-KV mode (FA-v2) and the row-layout partial mode
-// (fa_fwd_partial_ex: one chunk of query rows per launch in the multi-GPU path).
+// (fa_fwd_partial_ex: one chunk of query rows per launch in the multi-GPU path).  d = 128
+// with whole 64-key tiles runs fa_fwd16_kernel's strided form, every other case
+// fa_fwd_kernel's.
 #include "fa_fwd_kernel.hpp"
 #include "fa_fwd16_kernel.hpp"
 
@@ -12,11 +14,11 @@ template <typename T, typename PT, int D, int MODE>
 static hipError_t launch_strided_one(const FwdArgs& a, hipStream_t s) {
     const int64_t nblk = (int64_t)a.nqt * a.nsplit * a.BH;
     const int lds = fwd_lds_bytes(D);
-    // the multi-GPU chunks at d = 128 (row ranges of q, contiguous K / V, whole 64-key tiles):
-    // the 16x16x32 kernel, as the contiguous partial launch, so both give the same bits
-    if constexpr (D == 128 && MODE == kPartial) {
-        const bool kv_contig = a.k_stride[2] == D && a.k_stride[1] == a.Lk * D && a.k_stride[0] == a.H * a.Lk * D;
-        if (kv_contig && a.q_stride[2] == D && a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {
+    // d = 128 with whole 64-key tiles in every split (the multi-GPU q row ranges, [B, L, H, d]
+    // views, ...): the 16x16x32 kernel with strided addressing -- the same bits as the
+    // contiguous launch (round 4; the 32x32x16 kernel below sums in another order)
+    if constexpr (D == 128) {
+        if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();
         }

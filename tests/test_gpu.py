@@ -242,6 +242,28 @@ def test_strided_bshd_views(gpu, d):
         _gate(o, ref, torch.bfloat16)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+def test_strided_d128_matches_contiguous_bitwise(gpu, dtype):
+    """d = 128 with whole 64-key tiles: a [B, L, H, d] view runs fa_fwd16_kernel's strided form,
+    so it gives the contiguous launch's bits -- FA-v1 / tiled-d, the fused split-KV at the
+    library's plan, 4 and 1 key blocks per workgroup (the strided path used to
+    run the 32x32x16 kernel, whose summation order differs)."""
+    from exploring_flash_attention_amd import ops
+    B, H, L, d = 2, 3, 512, 128
+    q, k, v = (x.to(gpu) for x in _inputs(B, H, L, d, dtype, seed=77))
+    qs, ks, vs = (x.transpose(1, 2).contiguous().transpose(1, 2) for x in (q, k, v))
+    assert not qs.is_contiguous()
+    for fn in (lambda a, b, c, **kw: ops.attention_v1(a, b, c, **kw),
+               lambda a, b, c, **kw: ops.attention_tiled_d(a, b, c, 64, 64, **kw),
+               lambda a, b, c, **kw: ops.attention_v2(a, b, c, 2, **kw),
+               lambda a, b, c, **kw: ops.attention_v2(a, b, c, 2, blocks_per_workgroup=1, **kw)):
+        o_c = fn(q, k, v)
+        o_bshd = torch.empty((B, L, H, d), dtype=dtype, device=gpu)
+        fn(qs, ks, vs, out=o_bshd.transpose(1, 2))
+        torch.cuda.synchronize()
+        assert torch.equal(o_bshd.transpose(1, 2), o_c)
+
+
 def test_strided_views_without_kernel_layout(gpu):
     """Views the strided kernels cannot take (d not contiguous, k and v strided differently,
     fp64) run on contiguous copies: same results, out written in place."""

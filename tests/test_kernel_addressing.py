@@ -84,8 +84,8 @@ def replay(args, allocs, kernel16, strided=None, qstr=None, mode="final", pt_byt
     nkv = kv_end - kv_begin
     assert (nkv > 0).all(), "an empty split"
     ntiles = (nkv + bk - 1) // bk
-    if kernel16:
-        assert D == 128 and (nkv % 64 == 0).all() and strided is None
+    if kernel16:  # fa_fwd16_kernel: whole 64-key tiles (strided views too, round 4)
+        assert D == 128 and (nkv % 64 == 0).all()
     H = args.get("H", 1)
     # ---- Q descriptor
     q_tile0 = qt * KBQ
@@ -231,12 +231,14 @@ def test_multi_gpu_partials_in_bounds(W, L):
 
 
 @pytest.mark.parametrize("d", [32, 128, 256])
-def test_strided_blhd_views_in_bounds(d):
-    """[B, L, H, d] tensors viewed as [B, H, L, d] (fa_fwd_v1_ex strides {L*H*d, d, H*d})."""
-    B, H, L = 2, 4, 1000
+@pytest.mark.parametrize("L", [1000, 1024])
+def test_strided_blhd_views_in_bounds(d, L):
+    """[B, L, H, d] tensors viewed as [B, H, L, d] (fa_fwd_v1_ex strides {L*H*d, d, H*d}); d = 128
+    with whole 64-key tiles runs fa_fwd16_kernel's strided form."""
+    B, H = 2, 4
     st = (L * H * d, d, H * d)
     allocs = {n: _tensor(n, B, H, L, d) for n in "qkvo"}
-    replay(dict(_final_args(B, H, L, d)), allocs, False, strided=(st, st, st))
+    replay(dict(_final_args(B, H, L, d)), allocs, d == 128 and L % 64 == 0, strided=(st, st, st))
 
 
 def test_replay_catches_a_bad_decode():
