@@ -349,7 +349,7 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
         if (bq) *bq = fa::dtiled_rows_per_block();
         if (bk) *bk = keys_per_tile(e, d);
         if (threads) *threads = fa::kThreads;
-        if (lds_bytes) *lds_bytes = e == fa::Elem::F64 ? (64 + 2 * 16) * 129 * 8 + 4 * 16 * 17 * 8 : fa::dtiled_lds_bytes();
+        if (lds_bytes) *lds_bytes = e == fa::Elem::F64 ? (64 + 2 * 16) * 129 * 8 + 4 * 16 * 17 * 8 : fa::dtiled_lds_bytes((int)d);
         return ok();
     }
     if (bq) *bq = fa::kBQ;

@@ -24,10 +24,11 @@
 //   * Q^T fragments in registers for the whole loop (d/32 x 4 VGPRs: 64 at d = 512);
 //   * a query's 64 scores of a tile sit in 4 lanes (n, n+16, n+32, n+48): row max by two
 //     permlane swaps, row sums by a 16x16x32 MFMA with A = ones (as fa_fwd16_kernel.hpp);
-//   * LDS: a 3-slot ring of 16 KiB chunk images (the swizzled 8-row x 32-column subtile image of
-//     fa_device.hpp, row = 2 * chunk bytes), filled by LDS-DMA two chunks ahead of use: the
-//     chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one raw barrier per chunk, the DMA of
-//     chunk i+2 issued right after the barrier that retires chunk i-1's slot;
+//   * LDS: a ring of 16 KiB chunk images (the swizzled 8-row x 32-column subtile image of
+//     fa_device.hpp, row = 2 * chunk bytes; 4 slots at d = 384, 8 at d = 512), filled by LDS-DMA
+//     NSLOT-1 chunks ahead of use: the chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one
+//     raw barrier per chunk, the DMA of the next chunk issued right after the barrier that
+//     retires the previous chunk's slot; LDS reads one k-step / column block ahead;
 //   * registers: d = 384 fits 256 (two workgroups per CU), d = 512 takes 1 wave per SIMD.
 #include "fa_device.hpp"
 
@@ -38,25 +39,33 @@ constexpr int kDtRows = 16 * kDtWaves;  // query rows per workgroup
 constexpr int kDtBK = 64;               // keys per tile
 constexpr int kDtMaxChunk = 128;        // columns per LDS chunk at most
 constexpr int kDtSlotB = kDtBK * kDtMaxChunk * 2;
-constexpr int kDtSlots = 3;
+// ring slots: d = 384 keeps two workgroups per CU (4 x 16 KiB each), d = 512 runs one workgroup
+// per CU (one wave per SIMD by registers) and takes 8 slots -- 7 chunks in flight
+#ifndef FA_DT384_WPS
+#define FA_DT384_WPS 2  // waves per SIMD at d = 384 (2: two workgroups per CU)
+#endif
+constexpr int dt_wps(int d) { return d <= 384 ? FA_DT384_WPS : 1; }
+constexpr int dt_slots(int d) { return dt_wps(d) == 2 ? 4 : 8; }
 
 int dtiled_rows_per_block() { return kDtRows; }
-int dtiled_lds_bytes() { return kDtSlots * kDtSlotB; }
+int dtiled_lds_bytes(int d) { return dt_slots(d) * kDtSlotB; }
 
-// s_waitcnt vmcnt(n) for the DMA pieces a wave may leave in flight (n in {0, 1, 2, 4})
-__device__ __forceinline__ void wait_vm(int n) {
-    if (n >= 4)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (n == 2)
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if (n == 1)
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 31] (the DMA pieces allowed to stay in flight)
+__device__ __forceinline__ void wait_vm_le(int n) {
+#define FA_VM_CASE(k) \
+    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    switch (n < 0 ? 0 : n > 31 ? 31 : n) {
+        FA_VM_CASE(0) FA_VM_CASE(1) FA_VM_CASE(2) FA_VM_CASE(3) FA_VM_CASE(4) FA_VM_CASE(5) FA_VM_CASE(6)
+        FA_VM_CASE(7) FA_VM_CASE(8) FA_VM_CASE(9) FA_VM_CASE(10) FA_VM_CASE(11) FA_VM_CASE(12) FA_VM_CASE(13)
+        FA_VM_CASE(14) FA_VM_CASE(15) FA_VM_CASE(16) FA_VM_CASE(17) FA_VM_CASE(18) FA_VM_CASE(19) FA_VM_CASE(20)
+        FA_VM_CASE(21) FA_VM_CASE(22) FA_VM_CASE(23) FA_VM_CASE(24) FA_VM_CASE(25) FA_VM_CASE(26) FA_VM_CASE(27)
+        FA_VM_CASE(28) FA_VM_CASE(29) FA_VM_CASE(30) FA_VM_CASE(31)
+    }
+#undef FA_VM_CASE
 }
 
 template <typename T, int D>
-__global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArgs a) {
+__global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     static_assert(D % 128 == 0 && D > 256 && D <= 512, "d-tiled kernel: d = 384 or 512");
@@ -64,6 +73,7 @@ __global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArg
     constexpr int NDB = D / 16;  // O^T column blocks
     constexpr int NKB = 4;       // 16-key blocks per tile
     constexpr int ROWD = 2 * D;  // bytes per global row
+    constexpr int NSLOT = dt_slots(D);
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -79,7 +89,7 @@ __global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArg
 
     // chunk geometry (effective tiles: 32, 64 or 128 columns, dividing D)
     const int dq = a.d_tile_qk, dv = a.d_tile_v;
-    const int nqc = D / dq, nvc = D / dv, per_tile = nqc + nvc;
+    const int nqc = D / dq, per_tile = nqc + D / dv;
     const int kpc = dq / 32;          // QK^T k-steps per K chunk
     const int bpc = dv / 16;          // O^T column blocks per V chunk
     const int rowq = 2 * dq, rowv = 2 * dv;  // LDS image row bytes
@@ -111,35 +121,51 @@ __global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArg
         return row * ROWD + ch * 16;
     };
     const int kpw = dq / 32, vpw = dv / 32;  // pieces per wave of a K / V chunk (1, 2 or 4)
+    const int minpw = kpw < vpw ? kpw : vpw;
     int ksrc[4], vsrc[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         ksrc[p] = p < kpw ? src_off(wid * kpw + p, rowq) : 0;
         vsrc[p] = p < vpw ? src_off(wid * vpw + p, rowv) : 0;
     }
-    auto pieces = [&](int gi) { return gi >= total ? 0 : (gi % per_tile < nqc ? kpw : vpw); };
-    auto dma_chunk = [&](int gi) {
-        const int t = gi / per_tile, i = gi % per_tile;
-        const bool isk = i < nqc;
-        const int c = isk ? i : i - nqc, dt = isk ? dq : dv;
-        const int valid = nkv - t * kDtBK < kDtBK ? nkv - t * kDtBK : kDtBK;
+    // The chunk stream K(t, 0..) V(t, 0..) K(t+1, 0..) ... through an NSLOT ring, NSLOT-1 chunks
+    // ahead of use.  Issue state (tile, index in tile, slot) advances incrementally: no
+    // division per chunk (the scalar unit had been the busiest one).
+    int it = 0, ii = 0, islot = 0, issued = 0;
+    auto issue_next = [&]() {
+        if (issued >= total) return;
+        const bool isk = ii < nqc;
+        const int c = isk ? ii : ii - nqc, dt = isk ? dq : dv;
+        const int valid = nkv - it * kDtBK < kDtBK ? nkv - it * kDtBK : kDtBK;
         // rows past the last key read zeros (the range ends at the last valid row's chunk)
         const __amdgpu_buffer_rsrc_t rs = make_rsrc32(
-            (isk ? kbase : vbase) + (int64_t)t * kDtBK * ROWD + c * 2 * dt, (valid - 1) * ROWD + 2 * dt);
-        char* const slot = smem + (gi % kDtSlots) * kDtSlotB;
+            (isk ? kbase : vbase) + (int64_t)it * kDtBK * ROWD + c * 2 * dt, (valid - 1) * ROWD + 2 * dt);
+        char* const slot = smem + islot * kDtSlotB;
         const int pw = isk ? kpw : vpw;
 #pragma unroll
         for (int p = 0; p < 4; ++p)
             if (p < pw) dma16(rs, slot + (wid * pw + p) * 1024, isk ? ksrc[p] : vsrc[p], 0);
+        ++issued;
+        if (++ii == per_tile) {
+            ii = 0;
+            ++it;
+        }
+        if (++islot == NSLOT) islot = 0;
     };
-    // chunk gi becomes readable: its pieces landed (chunk gi+1 may stay in flight), every wave
-    // done with chunk gi-1 (whose slot the DMA of chunk gi+2 then refills)
-    auto advance = [&](int gi) {
-        wait_vm(pieces(gi + 1));
+    // chunk gi (the next to consume) becomes readable: its pieces landed -- the chunks issued
+    // after it may stay in flight, counted conservatively at the fewer pieces per chunk --, every
+    // wave done with chunk gi-1, whose slot the next issue then refills
+    int gi = 0, cslot = 0;
+    auto advance = [&]() {
+        const int after = issued - gi - 1;  // chunks issued after chunk gi
+        wait_vm_le(after * minpw);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (gi + 2 < total) dma_chunk(gi + 2);
-        return smem + (gi % kDtSlots) * kDtSlotB;
+        issue_next();
+        const char* const slot = smem + cslot * kDtSlotB;
+        ++gi;
+        if (++cslot == NSLOT) cslot = 0;
+        return slot;
     };
 
     // LDS read geometry (fa_fwd16_kernel.hpp): K rows read in the order rho(n), V^T by
@@ -165,26 +191,48 @@ __global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArg
     }
     const float c = a.scale_log2;
 
-    dma_chunk(0);
-    if (total > 1) dma_chunk(1);
-    int gi = 0;
+    // K fragments of one k-step (4 key blocks) / V^T operands of one column block (2 key
+    // steps x 2 reads), read ahead by one step inside a chunk
+    auto kread = [](u32x4 (&kf)[NKB], unsigned base, int rowq_) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[kb]) : "v"(base + kb * 16 * rowq_) : "memory");
+    };
+    auto vread = [](u32x2 (&vf)[4], unsigned vb, int rowv_) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[2 * kk]) : "v"(vb + kk * 32 * rowv_) : "memory");
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[2 * kk + 1]) : "v"(vb + kk * 32 * rowv_ + 16 * rowv_)
+                         : "memory");
+        }
+    };
+
+    for (int i = 0; i < NSLOT - 1; ++i) issue_next();
     const char* slot = smem;
     for (int t = 0; t < ntiles; ++t) {
         // ---- S^T = K Q^T over the d_tile_qk chunks of K
         f32x4 s[NKB];
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) s[kb] = f32x4{};
+        u32x4 kf[2][NKB];
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-            if (ks % kpc == 0) slot = advance(gi++);
-            const unsigned base = (unsigned)(size_t)slot + kl + (ks % kpc) * 512;
-            u32x4 kf[NKB];
+            if (ks % kpc == 0) {
+                slot = advance();
+                kread(kf[ks & 1], (unsigned)(size_t)slot + kl, rowq);
+            }
+            const bool ahead = ks + 1 < NKS && (ks + 1) % kpc != 0;  // next k-step in this chunk
+            if (ahead) {
+                kread(kf[(ks + 1) & 1], (unsigned)(size_t)slot + kl + ((ks + 1) % kpc) * 512, rowq);
+                asm volatile("s_waitcnt lgkmcnt(4)"
+                             : "+v"(kf[ks & 1][0]), "+v"(kf[ks & 1][1]), "+v"(kf[ks & 1][2]), "+v"(kf[ks & 1][3])::"memory");
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(kf[ks & 1][0]), "+v"(kf[ks & 1][1]), "+v"(kf[ks & 1][2]), "+v"(kf[ks & 1][3])::"memory");
+            }
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
-                asm volatile("ds_read_b128 %0, %1" : "=v"(kf[kb]) : "v"(base + kb * 16 * rowq) : "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3])::"memory");
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) s[kb] = M::mma16(__builtin_bit_cast(v8, kf[kb]), qf[ks], s[kb]);
+                s[kb] = M::mma16(__builtin_bit_cast(v8, kf[ks & 1][kb]), qf[ks], s[kb]);
         }
         // keys past the end (last tile only): score -inf
         if (nkv - t * kDtBK < kDtBK) {
@@ -226,17 +274,27 @@ __global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArg
         for (int kk = 0; kk < 2; ++kk) rs = M::mma16(ones, __builtin_bit_cast(v8, pbu[kk]), rs);
 
         // ---- O^T += V^T P^T over the d_tile_v chunks of V
+        u32x2 vf[2][4];
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-            if (db % bpc == 0) slot = advance(gi++);
-            const unsigned vb = (unsigned)(size_t)slot + ((db & 1) ? vl_o : vl_e) + 512 * ((db % bpc) >> 1);
+            if (db % bpc == 0) {
+                slot = advance();
+                vread(vf[db & 1], (unsigned)(size_t)slot + ((db & 1) ? vl_o : vl_e), rowv);
+            }
+            const bool ahead = db + 1 < NDB && (db + 1) % bpc != 0;
+            if (ahead) {
+                vread(vf[(db + 1) & 1],
+                      (unsigned)(size_t)slot + (((db + 1) & 1) ? vl_o : vl_e) + 512 * (((db + 1) % bpc) >> 1), rowv);
+                asm volatile("s_waitcnt lgkmcnt(4)"
+                             : "+v"(vf[db & 1][0]), "+v"(vf[db & 1][1]), "+v"(vf[db & 1][2]), "+v"(vf[db & 1][3])::"memory");
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(vf[db & 1][0]), "+v"(vf[db & 1][1]), "+v"(vf[db & 1][2]), "+v"(vf[db & 1][3])::"memory");
+            }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                u32x2 v0, v1;
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(vb + kk * 32 * rowv) : "memory");
-                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(vb + kk * 32 * rowv + 16 * rowv) : "memory");
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v0), "+v"(v1)::"memory");
-                const u32x4 vv = {v0[0], v0[1], v1[0], v1[1]};
+                const u32x4 vv = {vf[db & 1][2 * kk][0], vf[db & 1][2 * kk][1], vf[db & 1][2 * kk + 1][0],
+                                  vf[db & 1][2 * kk + 1][1]};
                 o[db] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[kk]), o[db]);
             }
         }
@@ -264,7 +322,7 @@ __global__ __launch_bounds__(256, D <= 384 ? 2 : 1) void fa_fwd_dt_kernel(FwdArg
 
 hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
-    const int lds = dtiled_lds_bytes();
+    const int lds = dtiled_lds_bytes(d);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kDtWaves * 64), lds, s, a);
         return hipGetLastError();

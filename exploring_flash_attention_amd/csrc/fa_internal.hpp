@@ -128,6 +128,6 @@ int fwd64_keys_per_tile();
 hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s);
 hipError_t launch_fwd64_dtiled(int d, const FwdArgs& a, hipStream_t s);
 int dtiled_rows_per_block();
-int dtiled_lds_bytes();
+int dtiled_lds_bytes(int d);
 
 }  // namespace fa

@@ -9,8 +9,9 @@ hipError_t launch_fwd64(int, Mode, const FwdArgs&, hipStream_t) { return hipErro
 hipError_t launch_combine64(int, const CombineArgs&, hipStream_t) { return hipErrorInvalidValue; }
 int fwd64_rows_per_block() { return 64; }
 int fwd64_keys_per_tile() { return 16; }
-hipError_t launch_fwd_dtiled(Elem, int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
+// (weak: a lite build of the d-tiled kernel links fa_fwd_dtiled.hip's real definitions)
+__attribute__((weak)) hipError_t launch_fwd_dtiled(Elem, int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
 hipError_t launch_fwd64_dtiled(int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
-int dtiled_rows_per_block() { return 64; }
-int dtiled_lds_bytes() { return 3 * 16384; }
+__attribute__((weak)) int dtiled_rows_per_block() { return 64; }
+__attribute__((weak)) int dtiled_lds_bytes(int d) { return (d <= 384 ? 4 : 8) * 16384; }
 }  // namespace fa
