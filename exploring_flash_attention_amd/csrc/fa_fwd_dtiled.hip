@@ -159,8 +159,9 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     auto advance = [&]() {
         const int after = issued - gi - 1;  // chunks issued after chunk gi
         wait_vm_le(after * minpw);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        // the barrier as inline asm with a memory clobber: no memory operation (the next DMA
+        // into the retired slot above all) may be moved across it, and no drain is implied
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         issue_next();
         const char* const slot = smem + cslot * kDtSlotB;
         ++gi;
