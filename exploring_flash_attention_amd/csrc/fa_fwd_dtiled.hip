@@ -28,7 +28,7 @@
 //     fa_device.hpp, row = 2 * chunk bytes; 4 slots at d = 384, 8 at d = 512), filled by LDS-DMA
 //     NSLOT-1 chunks ahead of use: the chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one
 //     raw barrier per chunk, the DMA of the next chunk issued right after the barrier that
-//     retires the previous chunk's slot; LDS reads one k-step / column block ahead;
+//     retires the previous chunk's slot;
 //   * registers: d = 384 fits 256 (two workgroups per CU), d = 512 takes 1 wave per SIMD.
 #include "fa_device.hpp"
 
@@ -193,7 +193,10 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     const float c = a.scale_log2;
 
     // K fragments of one k-step (4 key blocks) / V^T operands of one column block (2 key
-    // steps x 2 reads), read ahead by one step inside a chunk
+    // steps x 2 reads).  Each group is waited for right behind its reads: an asm read's result
+    // register must not be touched before its wait, and a read issued a step ahead left the
+    // compiler room to copy (spill) the not-yet-written register -- wrong results at d = 384
+    // (round 4)
     auto kread = [](u32x4 (&kf)[NKB], unsigned base, int rowq_) {
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
@@ -215,25 +218,14 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
         f32x4 s[NKB];
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) s[kb] = f32x4{};
-        u32x4 kf[2][NKB];
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-            if (ks % kpc == 0) {
-                slot = advance();
-                kread(kf[ks & 1], (unsigned)(size_t)slot + kl, rowq);
-            }
-            const bool ahead = ks + 1 < NKS && (ks + 1) % kpc != 0;  // next k-step in this chunk
-            if (ahead) {
-                kread(kf[(ks + 1) & 1], (unsigned)(size_t)slot + kl + ((ks + 1) % kpc) * 512, rowq);
-                asm volatile("s_waitcnt lgkmcnt(4)"
-                             : "+v"(kf[ks & 1][0]), "+v"(kf[ks & 1][1]), "+v"(kf[ks & 1][2]), "+v"(kf[ks & 1][3])::"memory");
-            } else {
-                asm volatile("s_waitcnt lgkmcnt(0)"
-                             : "+v"(kf[ks & 1][0]), "+v"(kf[ks & 1][1]), "+v"(kf[ks & 1][2]), "+v"(kf[ks & 1][3])::"memory");
-            }
+            if (ks % kpc == 0) slot = advance();
+            u32x4 kf[NKB];
+            kread(kf, (unsigned)(size_t)slot + kl + (ks % kpc) * 512, rowq);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3])::"memory");
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-                s[kb] = M::mma16(__builtin_bit_cast(v8, kf[ks & 1][kb]), qf[ks], s[kb]);
+            for (int kb = 0; kb < NKB; ++kb) s[kb] = M::mma16(__builtin_bit_cast(v8, kf[kb]), qf[ks], s[kb]);
         }
         // keys past the end (last tile only): score -inf
         if (nkv - t * kDtBK < kDtBK) {
@@ -275,27 +267,15 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
         for (int kk = 0; kk < 2; ++kk) rs = M::mma16(ones, __builtin_bit_cast(v8, pbu[kk]), rs);
 
         // ---- O^T += V^T P^T over the d_tile_v chunks of V
-        u32x2 vf[2][4];
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-            if (db % bpc == 0) {
-                slot = advance();
-                vread(vf[db & 1], (unsigned)(size_t)slot + ((db & 1) ? vl_o : vl_e), rowv);
-            }
-            const bool ahead = db + 1 < NDB && (db + 1) % bpc != 0;
-            if (ahead) {
-                vread(vf[(db + 1) & 1],
-                      (unsigned)(size_t)slot + (((db + 1) & 1) ? vl_o : vl_e) + 512 * (((db + 1) % bpc) >> 1), rowv);
-                asm volatile("s_waitcnt lgkmcnt(4)"
-                             : "+v"(vf[db & 1][0]), "+v"(vf[db & 1][1]), "+v"(vf[db & 1][2]), "+v"(vf[db & 1][3])::"memory");
-            } else {
-                asm volatile("s_waitcnt lgkmcnt(0)"
-                             : "+v"(vf[db & 1][0]), "+v"(vf[db & 1][1]), "+v"(vf[db & 1][2]), "+v"(vf[db & 1][3])::"memory");
-            }
+            if (db % bpc == 0) slot = advance();
+            u32x2 vf[4];
+            vread(vf, (unsigned)(size_t)slot + ((db & 1) ? vl_o : vl_e) + 512 * ((db % bpc) >> 1), rowv);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vf[0]), "+v"(vf[1]), "+v"(vf[2]), "+v"(vf[3])::"memory");
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                const u32x4 vv = {vf[db & 1][2 * kk][0], vf[db & 1][2 * kk][1], vf[db & 1][2 * kk + 1][0],
-                                  vf[db & 1][2 * kk + 1][1]};
+                const u32x4 vv = {vf[2 * kk][0], vf[2 * kk][1], vf[2 * kk + 1][0], vf[2 * kk + 1][1]};
                 o[db] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[kk]), o[db]);
             }
         }
