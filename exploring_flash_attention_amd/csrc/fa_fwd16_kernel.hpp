@@ -63,7 +63,7 @@ template <typename X> struct TypeTag { using type = X; };
 // descriptors take the row stride -- so a view gives the contiguous launch's bits.  (Partial
 // mode writes its own row layout; o_stride is not used there.)
 template <typename T, typename PT, int D, int MODE, bool STR = false>
-__global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
+__device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     static_assert(D == 128, "16x16x32 kernel: d = 128");
@@ -87,7 +87,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     char* const kring = smem;              // K ring: 2 slots
     char* const vring = smem + 2 * TILEB;  // V ring: 2 slots
 
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
     int qt, split;
     int64_t bh;
     decode_item(a, w, qt, split, bh);
@@ -95,6 +94,11 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n16 = lane & 15, g = lane >> 4;
+    // (FA_STAMPS diagnostic builds only, fa_fwd_kernel.hpp; slots as scripts/stamps.py reads them)
+    FA_STAMP_V(8, __builtin_amdgcn_s_memrealtime());
+    FA_STAMP(0);
+    FA_STAMP_V(6, __builtin_amdgcn_s_getreg(4 | (31 << 11)));
+    FA_STAMP_V(7, __builtin_amdgcn_s_getreg(20 | (31 << 11)));
     const int64_t kv_begin = (int64_t)split * a.kv_per_split;
     const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
     const int ntiles = (int)((kv_end - kv_begin) / kBK);
@@ -375,6 +379,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[qb][ks]));
     __syncthreads();
+    FA_STAMP(1);
     f32x4 sa[NKB][NQB], sb[NKB][NQB];
     float mx[NQB];
     qk_all(std::integral_constant<int, 0>{}, sa);
@@ -382,6 +387,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
     m[1] = mx[1];
     __syncthreads();  // K slot 0 is rewritten by step 0's DMA of K(2)
+    FA_STAMP(2);
 
     {
         using C0 = std::integral_constant<int, 0>;
@@ -402,6 +408,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         }
     }
 
+    FA_STAMP(3);
     // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n].  A 16-bit row is
     // stored 16 bytes per lane: dv blocks 2e and 2e+1 are paired by one v_permlane16_swap per
     // dword, lane group g then holds columns 32*e + 16*(g&1) + 8*(g>>1) .. +7.
@@ -459,6 +466,12 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
             const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
             if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o + o_head + q_row * orow, ov[qb], inv[qb]);
         }
+#if FA_STAMPS
+        FA_STAMP(4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FA_STAMP(5);
+        FA_STAMP_V(9, __builtin_amdgcn_s_memrealtime());
+#endif
     } else if constexpr (MODE == kPartial) {
 #pragma unroll
         for (int qb = 0; qb < NQB; ++qb) {
@@ -587,5 +600,59 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
         }
     }
 }
+
+template <typename T, typename PT, int D, int MODE, bool STR = false>
+__global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
+    fa_fwd16_item<T, PT, D, MODE, STR>(a, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+#if FA_DYN
+// EXPERIMENT (lite builds only, -DFA_DYN=1): persistent final-mode launch whose work items are
+// handed out dynamically, so that a slower XCD takes fewer of them.  The items (in xcd_remap
+// order) are cut into 8 ranges; the workgroups of XCD x (blockIdx % 8 == x under the observed
+// round-robin dispatch -- speed only, the claim protocol is placement-independent) first take one
+// static item of range x each, then claim the rest of range x through counter x, then steal from
+// the other ranges.  The last workgroup to exit clears the counters (one launch at a time per
+// process: diagnostic use only).
+__device__ unsigned g_fa_dyn[9 * 32];
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads, 2) void fa_fwd16_dyn_kernel(FwdArgs a, int nitems) {
+    __shared__ int s_item;
+    const int G = gridDim.x, b = blockIdx.x, xw = b & 7;
+    const int per = (nitems + 7) / 8;
+    auto lo_of = [&](int x) { return x * per < nitems ? x * per : nitems; };
+    auto hi_of = [&](int x) { return lo_of(x) + per < nitems ? lo_of(x) + per : nitems; };
+    auto nst_of = [&](int x) { return (G - x + 7) / 8; };  // static items of range x
+    int item = lo_of(xw) + (b >> 3) < hi_of(xw) ? lo_of(xw) + (b >> 3) : -1;
+    for (;;) {
+        if (item < 0) {
+            if (threadIdx.x == 0) {
+                int got = -1;
+                for (int k = 0; k < 8 && got < 0; ++k) {
+                    const int x = (xw + k) & 7;
+                    if (lo_of(x) + nst_of(x) >= hi_of(x)) continue;
+                    const unsigned t = __hip_atomic_fetch_add(&g_fa_dyn[32 * x], 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+                    const int cand = lo_of(x) + nst_of(x) + (int)t;
+                    if (cand < hi_of(x)) got = cand;
+                }
+                s_item = got;
+            }
+            __syncthreads();
+            item = s_item;
+            __syncthreads();
+            if (item < 0) break;
+        }
+        fa_fwd16_item<T, T, D, kFinal, false>(a, item);
+        item = -1;
+    }
+    if (threadIdx.x == 0) {
+        const unsigned done = __hip_atomic_fetch_add(&g_fa_dyn[32 * 8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done + 1 == (unsigned)G) {
+            for (int x = 0; x < 9; ++x) __hip_atomic_store(&g_fa_dyn[32 * x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+#endif
 
 }  // namespace fa

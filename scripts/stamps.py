@@ -123,6 +123,15 @@ def main():
     in_loop /= in_loop.sum()
     print(f"  CU time with 0 / 1 / 2 workgroups inside their KV loops: "
           f"{in_loop[0]:.1%} / {in_loop[1]:.1%} / {in_loop[2]:.1%}")
+    # per XCD: last end, and the clock its workgroups ran at (memtime cycles over realtime)
+    wclk = (s[:, 5] - s[:, 0]) / np.maximum(end - ent, 1e-3)  # cycles per us
+    step_cyc = (s[:, 3] - s[:, 2]) / ntiles
+    parts = []
+    for x in np.unique(xcc):
+        m_ = xcc == x
+        parts.append(f"x{int(x)}: end {end[m_].max():.1f} us, {np.median(wclk[m_]) / 1e3:.2f} GHz, "
+                     f"{np.median(step_cyc[m_]):.0f} cyc/step")
+    print("  per XCD: " + "; ".join(parts))
     total = end.max()
     print(f"  slot-time lost with < 2 resident workgroups (until the kernel's last end): "
           f"{np.mean([u + (total - le) for u, le in zip(under, last_end)]) / total:.1%} of 2 x span per CU"
