@@ -3,9 +3,6 @@
 // unit, so the two instantiation sets compile in parallel).
 #define FA_FWD_MAIN_TU
 #include "fa_fwd_kernel.hpp"
-#ifndef FA_DYN
-#define FA_DYN 0
-#endif
 #include "fa_fwd16_kernel.hpp"
 
 
@@ -21,13 +18,6 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     // the C5 partial pass +9 % over this file's 32x32x16 kernel)
     if constexpr (D == 128) {
         if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {  // no key tail in any split
-#if FA_DYN
-            if constexpr (MODE == kFinal && std::is_same_v<T, PT>) {
-                const int G = nblk < 512 ? (int)nblk : 512;
-                hipLaunchKernelGGL((fa_fwd16_dyn_kernel<T, D>), dim3((unsigned)G), dim3(kThreads), lds, s, a, (int)nblk);
-                return hipGetLastError();
-            }
-#endif
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();
         }

@@ -62,8 +62,15 @@ template <typename X> struct TypeTag { using type = X; };
 // (fa_fwd_partial_ex).  Only the global addressing changes -- the DMA source offsets and tile
 // descriptors take the row stride -- so a view gives the contiguous launch's bits.  (Partial
 // mode writes its own row layout; o_stride is not used there.)
-template <typename T, typename PT, int D, int MODE, bool STR = false>
-__device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w) {
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+// One work item (query tile, split, b*h) of the kernel; `at_loop_end` runs once, right after
+// the KV loop's last barrier (round 4's dynamic-claim experiment claimed its next item there;
+// measured and removed).
+template <typename T, typename PT, int D, int MODE, bool STR = false, typename Hook = NoHook>
+__device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, const Hook& at_loop_end = Hook{}) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     static_assert(D == 128, "16x16x32 kernel: d = 128");
@@ -409,6 +416,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w) {
     }
 
     FA_STAMP(3);
+    at_loop_end();
     // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n].  A 16-bit row is
     // stored 16 bytes per lane: dv blocks 2e and 2e+1 are paired by one v_permlane16_swap per
     // dword, lane group g then holds columns 32*e + 16*(g&1) + 8*(g>>1) .. +7.
@@ -605,54 +613,5 @@ template <typename T, typename PT, int D, int MODE, bool STR = false>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     fa_fwd16_item<T, PT, D, MODE, STR>(a, xcd_remap(blockIdx.x, gridDim.x));
 }
-
-#if FA_DYN
-// EXPERIMENT (lite builds only, -DFA_DYN=1): persistent final-mode launch whose work items are
-// handed out dynamically, so that a slower XCD takes fewer of them.  The items (in xcd_remap
-// order) are cut into 8 ranges; the workgroups of XCD x (blockIdx % 8 == x under the observed
-// round-robin dispatch -- speed only, the claim protocol is placement-independent) first take one
-// static item of range x each, then claim the rest of range x through counter x, then steal from
-// the other ranges.  The last workgroup to exit clears the counters (one launch at a time per
-// process: diagnostic use only).
-__device__ unsigned g_fa_dyn[9 * 32];
-template <typename T, int D>
-__global__ __launch_bounds__(kThreads, 2) void fa_fwd16_dyn_kernel(FwdArgs a, int nitems) {
-    __shared__ int s_item;
-    const int G = gridDim.x, b = blockIdx.x, xw = b & 7;
-    const int per = (nitems + 7) / 8;
-    auto lo_of = [&](int x) { return x * per < nitems ? x * per : nitems; };
-    auto hi_of = [&](int x) { return lo_of(x) + per < nitems ? lo_of(x) + per : nitems; };
-    auto nst_of = [&](int x) { return (G - x + 7) / 8; };  // static items of range x
-    int item = lo_of(xw) + (b >> 3) < hi_of(xw) ? lo_of(xw) + (b >> 3) : -1;
-    for (;;) {
-        if (item < 0) {
-            if (threadIdx.x == 0) {
-                int got = -1;
-                for (int k = 0; k < 8 && got < 0; ++k) {
-                    const int x = (xw + k) & 7;
-                    if (lo_of(x) + nst_of(x) >= hi_of(x)) continue;
-                    const unsigned t = __hip_atomic_fetch_add(&g_fa_dyn[32 * x], 1u, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-                    const int cand = lo_of(x) + nst_of(x) + (int)t;
-                    if (cand < hi_of(x)) got = cand;
-                }
-                s_item = got;
-            }
-            __syncthreads();
-            item = s_item;
-            __syncthreads();
-            if (item < 0) break;
-        }
-        fa_fwd16_item<T, T, D, kFinal, false>(a, item);
-        item = -1;
-    }
-    if (threadIdx.x == 0) {
-        const unsigned done = __hip_atomic_fetch_add(&g_fa_dyn[32 * 8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done + 1 == (unsigned)G) {
-            for (int x = 0; x < 9; ++x) __hip_atomic_store(&g_fa_dyn[32 * x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-#endif
 
 }  // namespace fa

@@ -6,9 +6,6 @@
 // with whole 64-key tiles runs fa_fwd16_kernel's strided form, every other case
 // fa_fwd_kernel's.
 #include "fa_fwd_kernel.hpp"
-#ifndef FA_DYN
-#define FA_DYN 0
-#endif
 #include "fa_fwd16_kernel.hpp"
 
 namespace fa {
