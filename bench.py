@@ -284,7 +284,7 @@ def c5_breakdown(torch, ops, fdist, dev, world, rank, barrier):
 # grouping forced (4 and 1 key blocks per workgroup: 4 / 16 partials per query tile) and the
 # automatic split; and two low-parallelism shapes -- the regime the reference's split-KV exists
 # for (flash_attention_v2/README.md:7-21): fewer query tiles than CUs, so the library itself
-# splits (2 and 4 partials per query tile) -- each against the same shape forced onto one
+# splits (4 partials per query tile each) -- each against the same shape forced onto one
 # workgroup per query tile (blocks_per_workgroup = all blocks).
 EXTRA_SHAPES = (
     # name, B, H, L, d, variant, kv_tiles_per_block, blocks_per_workgroup

@@ -235,9 +235,19 @@ int device_cus() {
 // loop at 0.88x the throughput of two; splitting B1 H2 L16384 (256 query tiles) into 8 partials
 // per tile to reach two per CU lost 10 %, B2 H2 L16384 into 4 lost 13 %: every partial pays a
 // prologue, an epilogue and its round trip through the workspace.  Splits pay when CUs idle.)
-int64_t wanted_partials(int64_t items, int64_t cap) {
+// Measured again in round 4 (scripts/split_sweep.py, profiles/r04/split_sweep.txt, d = 128
+// bf16): once every partial still runs >= 4096 keys its overheads amortise and the second
+// workgroup per CU pays after all -- B1 H1 L16384 4 partials per tile 121.8 us vs 2: 128.8;
+// B1 H2 L16384 2 vs 1: 225.8 vs 238.5 us -- while shorter partials do not (B1 H1 L8192 8 vs 4:
+// 49.1 vs 44.3 us; B1 H4 L4096 4 vs 2: 42.0 vs 41.5).  So for the d = 128 16-bit kernel: two
+// workgroups per CU when the partials stay that long, one per CU otherwise.
+int64_t wanted_partials(int64_t items, int64_t cap, int64_t L, int64_t d, fa::Elem e) {
     const int64_t ncu = device_cus();
     int64_t ns = items >= ncu ? 1 : (ncu + items - 1) / items;
+    if (d == 128 && (e == fa::Elem::BF16 || e == fa::Elem::F16)) {
+        const int64_t ns2 = items >= 2 * ncu ? 1 : (2 * ncu + items - 1) / items;
+        if (ns2 > ns && L / ns2 >= 4096) ns = ns2;
+    }
     return ns < cap ? ns : cap;
 }
 
@@ -248,7 +258,7 @@ int auto_kv_tiles(int64_t BH, int64_t L, int64_t d, fa::Elem e) {
     const int64_t bk = keys_per_tile(e, d);
     const int64_t ntiles = (L + bk - 1) / bk;
     const int64_t items = BH * ((L + rows_per_block(e, d) - 1) / rows_per_block(e, d));
-    const int64_t ns = wanted_partials(items, ntiles);
+    const int64_t ns = wanted_partials(items, ntiles, L, d, e);
     return (int)((ntiles + ns - 1) / ns);
 }
 
@@ -288,7 +298,7 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
     } else if (blocks_per_wg > 0) {
         p.group = blocks_per_wg < p.units ? blocks_per_wg : p.units;
     } else {
-        const int64_t ns = wanted_partials(items, p.units);
+        const int64_t ns = wanted_partials(items, p.units, L, d, e);
         p.group = (int)((p.units + ns - 1) / ns);  // equal groups (the last one may be shorter)
     }
     p.launched = (p.units + p.group - 1) / p.group;

@@ -79,7 +79,7 @@ def test_extra_shapes_split_where_the_library_splits():
     import bench
     from exploring_flash_attention_amd import ops
     shapes = {s[0]: s for s in bench.EXTRA_SHAPES}
-    for base, ppt in (("b1h1_l16k", 2), ("b1h2_l4k", 4)):
+    for base, ppt in (("b1h1_l16k", 4), ("b1h2_l4k", 4)):
         _, B, H, L, d, _, kvt, grp = shapes[base + "_splitkv"]
         assert grp is None and ops.v2_split_plan(B, H, L, d, kvt)[2] == ppt
         _, B, H, L, d, _, kvt, grp = shapes[base + "_unsplit"]

@@ -167,13 +167,17 @@ def test_workspace_size_and_v2_checks():
     assert lib.fa_fwd_v2_split_plan(1, 1, 8192, 128, 4, AUTO, L.FA_DTYPE_BF16, ctypes.byref(kb), ctypes.byref(g),
                                     ctypes.byref(p)) == 0
     assert (kb.value, g.value, p.value) == (32, 8, 4)
-    # 256 query tiles already occupy every CU: no split (measured: 8 partials there lose 10 %)
+    # 256 query tiles already occupy every CU once; a second workgroup per CU pays when each
+    # partial keeps >= 4096 keys (measured round 4, profiles/r04/split_sweep.txt): 2 partials
+    # of 8192 keys here, 4 of 4096 at 128 query tiles
     assert lib.fa_fwd_v2_split_plan(1, 2, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
-                                    ctypes.byref(p)) == 0 and p.value == 1
-    # 128 query tiles: two partials each; 100 query tiles: ceil(256 / 100) = 3 (its 50 key blocks in
-    # groups of ceil(50 / 3) = 17)
-    assert lib.fa_fwd_v2_split_plan(1, 1, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
                                     ctypes.byref(p)) == 0 and (g.value, p.value) == (32, 2)
+    assert lib.fa_fwd_v2_split_plan(1, 1, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                    ctypes.byref(p)) == 0 and (g.value, p.value) == (16, 4)
+    # ... but not below 4096 keys: 100 query tiles: ceil(256 / 100) = 3 (its 50 key blocks in
+    # groups of ceil(50 / 3) = 17; 6 partials would hold 2133 keys); B4 H2 L16384: 1024 tiles
+    assert lib.fa_fwd_v2_split_plan(4, 2, 16384, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
+                                    ctypes.byref(p)) == 0 and p.value == 1
     assert lib.fa_fwd_v2_split_plan(1, 1, 12800, 128, 4, AUTO, L.FA_DTYPE_BF16, None, ctypes.byref(g),
                                     ctypes.byref(p)) == 0 and (g.value, p.value) == (17, 3)
     assert lib.fa_fwd_v2_workspace_size(1, 1, 100, 64, 1, L.FA_DTYPE_FP16, L.FA_DTYPE_FP32,
