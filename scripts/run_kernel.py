@@ -4,7 +4,8 @@
 
 configs: c2, c3 (FA-v1), c4 (split-KV, KV_TILES_PER_BLOCK = 4, the library's grouping), c4g4 /
 c4g1 (C4 with 4 / 1 key blocks per workgroup: 4 / 16 partials per query tile), b1h1l16k (a
-shape the library splits itself: 2 partials per query tile), b1h1l16k_unsplit (the same shape,
+shape the library splits itself: 4 partials per query tile since round 4's plan, 2 before),
+b1h2l16k (2 partials per tile; 1 before), b1h1l16k_unsplit (the same shape,
 one workgroup per query tile), b1h2l4k / _unsplit (4 partials per tile / none), c5 (one rank's
 C5 partial kernel shape, FA-v1 form), d384 / d512 (the d-tiled kernel at B32 H8 L1024).
 """
@@ -19,7 +20,8 @@ from exploring_flash_attention_amd import ops  # noqa: E402
 CFG = {"c2": (32, 8, 1024, 32, "v1", None), "c3": (32, 8, 1024, 128, "v1", None),
        "c4": (32, 8, 4096, 128, "v2", None), "c4g4": (32, 8, 4096, 128, "v2", 4),
        "c4g1": (32, 8, 4096, 128, "v2", 1), "b1h1l16k": (1, 1, 16384, 128, "v2", None),
-       "b1h1l16k_unsplit": (1, 1, 16384, 128, "v2", 64), "c5": (32, 8, 16384, 128, "v1", None),
+       "b1h1l16k_unsplit": (1, 1, 16384, 128, "v2", 64),
+       "b1h2l16k": (1, 2, 16384, 128, "v2", None), "c5": (32, 8, 16384, 128, "v1", None),
        "b1h2l4k": (1, 2, 4096, 128, "v2", None), "b1h2l4k_unsplit": (1, 2, 4096, 128, "v2", 16),
        "d384": (32, 8, 1024, 384, "td", None), "d512": (32, 8, 1024, 512, "td", None)}
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
