@@ -302,6 +302,7 @@ EXTRA_SHAPES = (
     ("b1h2_l4k_unsplit", 1, 2, 4096, 128, "v2", 4, "all"),
 )
 SPLIT_PAIRS = ("b1h1_l16k", "b1h2_l4k")
+EXTRA_SETTLE_S = 0.1  # untimed back-to-back launches of each extra shape before its window
 
 
 def single_gpu_extras(torch, ops, dev, barrier, names=None):
@@ -333,6 +334,11 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
                        partials_per_tile=plan[2], workspace_bytes=nb)
         f = flops(B, H, L, d)
         n = max(10, min(50, int(2e13 / f)))  # >= ~20 TFLOP of work per timing window
+        # each shape's own clock settle: the chip's clock after the previous shape (a
+        # low-power one boosts it, a hot one holds it down) otherwise carries into this window
+        # (C4 read 1.84 ms after the d = 512 shape and 1.74 ms for the same kernel and grid as
+        # c4_splitkv_auto; profiles/r04/bench_driver_cmd_g.json)
+        clock_settle(torch, st, EXTRA_SETTLE_S)
         _, ems = time_step(torch, st, n, max(3, n // 3), barrier)
         ms = ems / n
         rec.update(ms=round(ms, 4), tflops=round(f / (ms * 1e-3) / 1e12, 1),

@@ -25,11 +25,11 @@
 //   * a query's 64 scores of a tile sit in 4 lanes (n, n+16, n+32, n+48): row max by two
 //     permlane swaps, row sums by a 16x16x32 MFMA with A = ones (as fa_fwd16_kernel.hpp);
 //   * LDS: a ring of 16 KiB chunk images (the swizzled 8-row x 32-column subtile image of
-//     fa_device.hpp, row = 2 * chunk bytes; 4 slots at d = 384, 8 at d = 512), filled by LDS-DMA
+//     fa_device.hpp, row = 2 * chunk bytes; 4 slots), filled by LDS-DMA
 //     NSLOT-1 chunks ahead of use: the chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one
 //     raw barrier per chunk, the DMA of the next chunk issued right after the barrier that
 //     retires the previous chunk's slot;
-//   * registers: d = 384 fits 256 (two workgroups per CU), d = 512 takes 1 wave per SIMD.
+//   * registers: d = 384 and 512 both fit 256 (two workgroups per CU: 224 / 252 VGPRs).
 #include "fa_device.hpp"
 
 namespace fa {
@@ -39,32 +39,59 @@ constexpr int kDtRows = 16 * kDtWaves;  // query rows per workgroup
 constexpr int kDtBK = 64;               // keys per tile
 constexpr int kDtMaxChunk = 128;        // columns per LDS chunk at most
 constexpr int kDtSlotB = kDtBK * kDtMaxChunk * 2;
-// ring slots: d = 384 keeps two workgroups per CU (4 x 16 KiB each), d = 512 runs one workgroup
-// per CU (one wave per SIMD by registers) and takes 8 slots -- 7 chunks in flight
+// ring slots: two workgroups per CU (one wave per SIMD each), 4 x 16 KiB each; one workgroup per
+// CU would take 8 slots -- 7 chunks in flight -- and measured slower (d = 512: 903 vs 672 us at
+// B32 H8 L1024, profiles/r04/ab_dtiled_g.log)
 #ifndef FA_DT384_WPS
 #define FA_DT384_WPS 2  // waves per SIMD at d = 384 (2: two workgroups per CU)
 #endif
-constexpr int dt_wps(int d) { return d <= 384 ? FA_DT384_WPS : 1; }
+#ifndef FA_DT512_WPS
+#define FA_DT512_WPS 2  // waves per SIMD at d = 512 (2: 252 VGPRs, no scratch; 1: 8 ring slots)
+#endif
+constexpr int dt_wps(int d) { return d <= 384 ? FA_DT384_WPS : FA_DT512_WPS; }
 constexpr int dt_slots(int d) { return dt_wps(d) == 2 ? 4 : 8; }
 
 int dtiled_rows_per_block() { return kDtRows; }
 int dtiled_lds_bytes(int d) { return dt_slots(d) * kDtSlotB; }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 31] (the DMA pieces allowed to stay in flight)
-__device__ __forceinline__ void wait_vm_le(int n) {
-#define FA_VM_CASE(k) \
-    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    switch (n < 0 ? 0 : n > 31 ? 31 : n) {
-        FA_VM_CASE(0) FA_VM_CASE(1) FA_VM_CASE(2) FA_VM_CASE(3) FA_VM_CASE(4) FA_VM_CASE(5) FA_VM_CASE(6)
-        FA_VM_CASE(7) FA_VM_CASE(8) FA_VM_CASE(9) FA_VM_CASE(10) FA_VM_CASE(11) FA_VM_CASE(12) FA_VM_CASE(13)
-        FA_VM_CASE(14) FA_VM_CASE(15) FA_VM_CASE(16) FA_VM_CASE(17) FA_VM_CASE(18) FA_VM_CASE(19) FA_VM_CASE(20)
-        FA_VM_CASE(21) FA_VM_CASE(22) FA_VM_CASE(23) FA_VM_CASE(24) FA_VM_CASE(25) FA_VM_CASE(26) FA_VM_CASE(27)
-        FA_VM_CASE(28) FA_VM_CASE(29) FA_VM_CASE(30) FA_VM_CASE(31)
-    }
-#undef FA_VM_CASE
+// s_waitcnt vmcnt(N), N a compile-time count of DMA pieces allowed to stay in flight
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T, int D>
+// One 1 KiB LDS-DMA piece (buffer_load_dwordx4 ... lds; M0 = the wave's LDS destination), as
+// inline asm so that the compiler does not see it: for a compiler-visible LDS-DMA it places an
+// s_waitcnt vmcnt(0) -- every piece in flight -- before each ds_read_b64_tr_b16 builtin (it
+// cannot tell the transposed read from a read of the bytes being written), which would drain
+// the ring at every V chunk.  The ring's own vmcnt waits and barriers order the DMAs and the
+// reads.  M0 carries no other value in these kernels (no LDS-DMA builtin, no movrel).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t rs, const char* lds, int voff) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lds);
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(rs)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// The chunk stream of one (d, d_tile_qk, d_tile_v): per 64-key tile NQC K chunks of DQ columns
+// then NVC V chunks of DV columns, each chunk 1 KiB pieces, DQ / 32 (DV / 32) per wave.
+template <int D, int DQ, int DV, int NSLOT>
+struct DtStream {
+    static constexpr int NQC = D / DQ, NVC = D / DV, PER_TILE = NQC + NVC;
+    static constexpr int KPW = DQ / 32, VPW = DV / 32;
+    static constexpr int pieces(int pos) { return pos < NQC ? KPW : VPW; }
+    // pieces of the NSLOT - 2 chunks issued after the chunk at position pos (steady state)
+    static constexpr int after(int pos) {
+        int n = 0;
+        for (int i = 1; i <= NSLOT - 2; ++i) n += pieces((pos + i) % PER_TILE);
+        return n;
+    }
+};
+
+template <typename T, int D, int DQ, int DV>
 __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
@@ -87,12 +114,13 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     const int nkv = (int)a.Lk;
     const int ntiles = (nkv + kDtBK - 1) / kDtBK;
 
-    // chunk geometry (effective tiles: 32, 64 or 128 columns, dividing D)
-    const int dq = a.d_tile_qk, dv = a.d_tile_v;
-    const int nqc = D / dq, per_tile = nqc + D / dv;
-    const int kpc = dq / 32;          // QK^T k-steps per K chunk
-    const int bpc = dv / 16;          // O^T column blocks per V chunk
-    const int rowq = 2 * dq, rowv = 2 * dv;  // LDS image row bytes
+    // chunk geometry (effective tiles: 32, 64 or 128 columns, dividing D; one instantiation
+    // per pair, so every chunk boundary and every DMA count below is a compile-time constant)
+    using S = DtStream<D, DQ, DV, NSLOT>;
+    constexpr int nqc = S::NQC, per_tile = S::PER_TILE;
+    constexpr int kpc = DQ / 32;          // QK^T k-steps per K chunk
+    constexpr int bpc = DV / 16;          // O^T column blocks per V chunk
+    constexpr int rowq = 2 * DQ, rowv = 2 * DV;  // LDS image row bytes
     const int total = ntiles * per_tile;
 
     // Q^T fragments (B operand): lane (g, n) holds Q[16*wid + n][32*ks + 8*pg .. +7], the
@@ -120,52 +148,50 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
         const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
         return row * ROWD + ch * 16;
     };
-    const int kpw = dq / 32, vpw = dv / 32;  // pieces per wave of a K / V chunk (1, 2 or 4)
-    const int minpw = kpw < vpw ? kpw : vpw;
-    int ksrc[4], vsrc[4];
+    constexpr int kpw = S::KPW, vpw = S::VPW;  // pieces per wave of a K / V chunk (1, 2 or 4)
+    int ksrc[kpw], vsrc[vpw];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        ksrc[p] = p < kpw ? src_off(wid * kpw + p, rowq) : 0;
-        vsrc[p] = p < vpw ? src_off(wid * vpw + p, rowv) : 0;
-    }
+    for (int p = 0; p < kpw; ++p) ksrc[p] = src_off(wid * kpw + p, rowq);
+#pragma unroll
+    for (int p = 0; p < vpw; ++p) vsrc[p] = src_off(wid * vpw + p, rowv);
     // The chunk stream K(t, 0..) V(t, 0..) K(t+1, 0..) ... through an NSLOT ring, NSLOT-1 chunks
-    // ahead of use.  Issue state (tile, index in tile, slot) advances incrementally: no
-    // division per chunk (the scalar unit had been the busiest one).
-    int it = 0, ii = 0, islot = 0, issued = 0;
-    auto issue_next = [&]() {
-        if (issued >= total) return;
-        const bool isk = ii < nqc;
-        const int c = isk ? ii : ii - nqc, dt = isk ? dq : dv;
+    // ahead of use.  Chunk gi = t * per_tile + pos sits in slot gi % NSLOT (`cslot`, carried as
+    // it advances); pos is static at every use, so is the chunk's kind and column offset.
+    auto issue = [&](auto pos_c, int it, int islot) {
+        constexpr int pos = decltype(pos_c)::value;
+        constexpr bool isk = pos < nqc;
+        constexpr int c = isk ? pos : pos - nqc, dt = isk ? DQ : DV;
         const int valid = nkv - it * kDtBK < kDtBK ? nkv - it * kDtBK : kDtBK;
         // rows past the last key read zeros (the range ends at the last valid row's chunk)
         const __amdgpu_buffer_rsrc_t rs = make_rsrc32(
             (isk ? kbase : vbase) + (int64_t)it * kDtBK * ROWD + c * 2 * dt, (valid - 1) * ROWD + 2 * dt);
         char* const slot = smem + islot * kDtSlotB;
-        const int pw = isk ? kpw : vpw;
+        constexpr int pw = isk ? kpw : vpw;
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-            if (p < pw) dma16(rs, slot + (wid * pw + p) * 1024, isk ? ksrc[p] : vsrc[p], 0);
-        ++issued;
-        if (++ii == per_tile) {
-            ii = 0;
-            ++it;
-        }
-        if (++islot == NSLOT) islot = 0;
+        for (int p = 0; p < pw; ++p) dma16_asm(rs, slot + (wid * pw + p) * 1024, isk ? ksrc[p] : vsrc[p]);
     };
-    // chunk gi (the next to consume) becomes readable: its pieces landed -- the chunks issued
-    // after it may stay in flight, counted conservatively at the fewer pieces per chunk --, every
-    // wave done with chunk gi-1, whose slot the next issue then refills
-    int gi = 0, cslot = 0;
-    auto advance = [&]() {
-        const int after = issued - gi - 1;  // chunks issued after chunk gi
-        wait_vm_le(after * minpw);
+    // chunk gi = t * per_tile + pos (the next to consume) becomes readable: its pieces landed
+    // (in the steady state exactly S::after(pos) pieces were issued after it; near the end of
+    // the stream fewer, and the wait drains), every wave is done with chunk gi-1, whose slot
+    // the chunk gi + NSLOT - 1 then refills
+    int cslot = 0;
+    auto advance = [&](auto pos_c, int t) {
+        constexpr int pos = decltype(pos_c)::value;
+        const int gi = t * per_tile + pos;
+        if (gi + NSLOT - 1 <= total)
+            wait_vm<S::after(pos)>();
+        else
+            wait_vm<0>();
         // the barrier as inline asm with a memory clobber: no memory operation (the next DMA
         // into the retired slot above all) may be moved across it, and no drain is implied
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        issue_next();
+        if (gi + NSLOT - 1 < total) {
+            constexpr int npos = (pos + NSLOT - 1) % per_tile;
+            issue(std::integral_constant<int, npos>{}, t + (pos + NSLOT - 1) / per_tile,
+                  cslot == 0 ? NSLOT - 1 : cslot - 1);
+        }
         const char* const slot = smem + cslot * kDtSlotB;
-        ++gi;
-        if (++cslot == NSLOT) cslot = 0;
+        cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
         return slot;
     };
 
@@ -193,40 +219,55 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     const float c = a.scale_log2;
 
     // K fragments of one k-step (4 key blocks) / V^T operands of one column block (2 key
-    // steps x 2 reads).  Each group is waited for right behind its reads: an asm read's result
-    // register must not be touched before its wait, and a read issued a step ahead left the
-    // compiler room to copy (spill) the not-yet-written register -- wrong results at d = 384
-    // (round 4)
-    auto kread = [](u32x4 (&kf)[NKB], unsigned base, int rowq_) {
+    // steps x 2 reads), as compiler-visible LDS loads: the compiler places the lgkmcnt waits and
+    // may issue the reads of later k-steps of a chunk ahead of earlier MFMAs (it inserts no
+    // vmcnt wait for the LDS-DMA -- the ring's own waits and barriers order those, and the
+    // barrier's memory clobber keeps every read between its chunk's two barriers).  (Round 4's
+    // first build used asm reads, each group waited right behind its issue: a read issued ahead
+    // had let the compiler copy its not-yet-written register -- wrong results at d = 384; the
+    // exposed latency then cost 15 k cycles per 64-key step at d = 512.)
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    auto kread = [](u32x4 (&kf)[NKB], const char* base, int rowq_) {
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[kb]) : "v"(base + kb * 16 * rowq_) : "memory");
+        for (int kb = 0; kb < NKB; ++kb) kf[kb] = *(const u32x4*)(base + kb * 16 * rowq_);
     };
-    auto vread = [](u32x2 (&vf)[4], unsigned vb, int rowv_) {
+    auto vread = [](u32x2 (&vf)[4], const char* vb, int rowv_) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[2 * kk]) : "v"(vb + kk * 32 * rowv_) : "memory");
-            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[2 * kk + 1]) : "v"(vb + kk * 32 * rowv_ + 16 * rowv_)
-                         : "memory");
+            vf[2 * kk] = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                       (lds_s16x4*)(vb + kk * 32 * rowv_)));
+            vf[2 * kk + 1] = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                           (lds_s16x4*)(vb + kk * 32 * rowv_ + 16 * rowv_)));
         }
     };
 
-    for (int i = 0; i < NSLOT - 1; ++i) issue_next();
+    // The first NSLOT - 1 chunks (positions and tiles static; total >= per_tile >= NSLOT - 1):
+    // chunk 0, then a fence that has the compiler wait for Q (vmcnt(0): it counts only the Q
+    // loads, and chunk 0 went out before them), then the rest in flight.  Without the fence the
+    // compiler places a wait for Q before each k-step's first MFMA, inside the loop, where its
+    // counts would drain the ring.
+    static_assert(NSLOT - 1 <= per_tile, "the first ring fill lies within tile 0");
+    issue(std::integral_constant<int, 0>{}, 0, 0);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));
+    static_for<NSLOT - 2>([&](auto i_c) {
+        constexpr int i = decltype(i_c)::value + 1;
+        issue(std::integral_constant<int, i>{}, 0, i);
+    });
     const char* slot = smem;
     for (int t = 0; t < ntiles; ++t) {
         // ---- S^T = K Q^T over the d_tile_qk chunks of K
         f32x4 s[NKB];
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) s[kb] = f32x4{};
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            if (ks % kpc == 0) slot = advance();
+        static_for<NKS>([&](auto ks_c) {
+            constexpr int ks = decltype(ks_c)::value;
+            if constexpr (ks % kpc == 0) slot = advance(std::integral_constant<int, ks / kpc>{}, t);
             u32x4 kf[NKB];
-            kread(kf, (unsigned)(size_t)slot + kl + (ks % kpc) * 512, rowq);
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3])::"memory");
+            kread(kf, slot + kl + (ks % kpc) * 512, rowq);
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) s[kb] = M::mma16(__builtin_bit_cast(v8, kf[kb]), qf[ks], s[kb]);
-        }
+        });
         // keys past the end (last tile only): score -inf
         if (nkv - t * kDtBK < kDtBK) {
 #pragma unroll
@@ -267,18 +308,17 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
         for (int kk = 0; kk < 2; ++kk) rs = M::mma16(ones, __builtin_bit_cast(v8, pbu[kk]), rs);
 
         // ---- O^T += V^T P^T over the d_tile_v chunks of V
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-            if (db % bpc == 0) slot = advance();
+        static_for<NDB>([&](auto db_c) {
+            constexpr int db = decltype(db_c)::value;
+            if constexpr (db % bpc == 0) slot = advance(std::integral_constant<int, nqc + db / bpc>{}, t);
             u32x2 vf[4];
-            vread(vf, (unsigned)(size_t)slot + ((db & 1) ? vl_o : vl_e) + 512 * ((db % bpc) >> 1), rowv);
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vf[0]), "+v"(vf[1]), "+v"(vf[2]), "+v"(vf[3])::"memory");
+            vread(vf, slot + ((db & 1) ? vl_o : vl_e) + 512 * ((db % bpc) >> 1), rowv);
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
                 const u32x4 vv = {vf[2 * kk][0], vf[2 * kk][1], vf[2 * kk + 1][0], vf[2 * kk + 1][1]};
                 o[db] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[kk]), o[db]);
             }
-        }
+        });
     }
 
     // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query n]; dv blocks 2e and 2e+1 are
@@ -301,19 +341,38 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     }
 }
 
-hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s) {
-    const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
-    const int lds = dtiled_lds_bytes(d);
+template <typename T, int D>
+static hipError_t launch_dt(const FwdArgs& a, const dim3& grid, int lds, hipStream_t s) {
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kDtWaves * 64), lds, s, a);
         return hipGetLastError();
     };
+    auto pick_v = [&](auto dq_c) -> hipError_t {
+        constexpr int DQ = decltype(dq_c)::value;
+        switch (a.d_tile_v) {
+            case 32: return go(fa_fwd_dt_kernel<T, D, DQ, 32>);
+            case 64: return go(fa_fwd_dt_kernel<T, D, DQ, 64>);
+            case 128: return go(fa_fwd_dt_kernel<T, D, DQ, 128>);
+        }
+        return hipErrorInvalidValue;
+    };
+    switch (a.d_tile_qk) {
+        case 32: return pick_v(std::integral_constant<int, 32>{});
+        case 64: return pick_v(std::integral_constant<int, 64>{});
+        case 128: return pick_v(std::integral_constant<int, 128>{});
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s) {
+    const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
+    const int lds = dtiled_lds_bytes(d);
     if (t == Elem::BF16) {
-        if (d == 384) return go(fa_fwd_dt_kernel<__bf16, 384>);
-        if (d == 512) return go(fa_fwd_dt_kernel<__bf16, 512>);
+        if (d == 384) return launch_dt<__bf16, 384>(a, grid, lds, s);
+        if (d == 512) return launch_dt<__bf16, 512>(a, grid, lds, s);
     } else if (t == Elem::F16) {
-        if (d == 384) return go(fa_fwd_dt_kernel<_Float16, 384>);
-        if (d == 512) return go(fa_fwd_dt_kernel<_Float16, 512>);
+        if (d == 384) return launch_dt<_Float16, 384>(a, grid, lds, s);
+        if (d == 512) return launch_dt<_Float16, 512>(a, grid, lds, s);
     }
     return hipErrorInvalidValue;
 }

@@ -14,7 +14,9 @@ pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   src=$CS/fa_fwd_dtiled.hip; case $flags in *DT_OLD*) src=$CS/fa_fwd_dtiled_old.hip ;; esac
-  ( /opt/rocm/bin/hipcc $FL $flags -x hip -c $src -o /tmp/fa_lite/$name.dt.o &&
+  # a flag set naming FA_DT_AGPR builds the d-tiled file without --amdgpu-mfma-vgpr-form
+  FLD=$FL; case $flags in *FA_DT_AGPR*) FLD=${FL/ -mllvm --amdgpu-mfma-vgpr-form/} ;; esac
+  ( /opt/rocm/bin/hipcc $FLD $flags -x hip -c $src -o /tmp/fa_lite/$name.dt.o &&
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/$name.so /tmp/fa_lite/$name.dt.o /tmp/fa_lite/fwd128.o \
         /tmp/fa_lite/capi.o /tmp/fa_lite/stubs.o && echo "built $name ($flags)" ) &
   pids+=($!)
