@@ -105,3 +105,54 @@ def test_splitkv_eight_ranks_c5_length(tmp_path):
     all 16384 query rows, the exchange, the combine and the all-gather, checked against the
     fp64 oracle on 32 sampled rows of every rank's chunk (first and last included)."""
     _run(tmp_path, 8, "bfloat16", (1, 2, 16384, 128), sampled=True)
+
+
+def _native_worker(rank, world, port, path):
+    """One rank per GPU over RCCL: the native C-ABI forward (fa_fwd_v2_dist: pipelined
+    per-destination partial launches, the shifted send/recv steps, combine, all-gather) against
+    the Python paths (all-to-all and pipelined send/recv) over the same RCCL group, bit for bit,
+    and against the fp64 oracle on sampled rows."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    from exploring_flash_attention_amd import dist as fdist
+    g = torch.Generator().manual_seed(0)
+    B, H, L, d = 2, 4, 2048, 128
+    q, k, v = (torch.randn(B, H, L, d, generator=g).to(torch.bfloat16) for _ in range(3))
+    lo, hi = fdist.shard_bounds(L, world, rank)
+    dev = torch.device("cuda", rank)
+    qg = q.to(dev)
+    ks, vs = k[:, :, lo:hi].contiguous().to(dev), v[:, :, lo:hi].contiguous().to(dev)
+    comm = fdist.RcclComm()
+    nat_local = fdist.splitkv_attention_native(qg, ks, vs, comm)
+    nat_full = fdist.splitkv_attention_native(qg, ks, vs, comm, gather=True)
+    py_full = fdist.splitkv_attention(qg, ks, vs, overlap=False, gather=True)
+    py_ovl = fdist.splitkv_attention(qg, ks, vs, gather=True)  # pipelined send/recv over RCCL
+    torch.cuda.synchronize()
+    comm.close()
+    rows = np.unique(np.linspace(0, L - 1, 64).round().astype(int))
+    ref = _rows_ref(q, k, v, rows)
+    err = np.abs(nat_full[:, :, torch.from_numpy(rows).to(dev)].double().cpu().numpy() - ref).max()
+    same = bool(torch.equal(nat_full, py_full)) and bool(torch.equal(nat_full, py_ovl))
+    own = bool(torch.equal(nat_local, nat_full[:, :, rank * (L // world):(rank + 1) * (L // world)]))
+    with open(f"{path}.{rank}", "w") as f:
+        f.write(f"{err}|{same}|{own}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300, method="thread")
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_native_rccl_exchange_one_gpu_per_rank(tmp_path, world):
+    """The native RCCL exchange at W > 1 (include/fa_mi355x_dist.h), which needs one device per
+    rank: skipped on boxes with fewer GPUs (the CPU schedule test, tests/test_dist_schedule.py,
+    covers its step pairing, offsets and failure latch everywhere)."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs, {torch.cuda.device_count()} visible")
+    port, path = _free_port(), str(tmp_path / "res")
+    mp.start_processes(_native_worker, args=(world, port, path), nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        err, same, own = open(f"{path}.{r}").read().split("|")
+        assert float(err) < 6e-3, (r, err)
+        assert same == "True", f"rank {r}: native and Python split-KV differ"
+        assert own == "True", f"rank {r}: the local rows are not the gathered ones"
