@@ -647,7 +647,9 @@ def test_scaled_partials_near_bf16_max(gpu):
 # head dims past one tile: the d-tiled kernels (csrc/fa_fwd_dtiled.hip, fa_fwd64.hip)
 # ----------------------------------------------------------------------------------------
 
-WIDE_TILES = [(32, 32), (64, 128), (128, 64), (100, 48), (512, 512)]
+# every (d_tile_qk, d_tile_v) instantiation of the 16-bit d-tiled kernel (32 / 64 / 128 columns
+# each), a ragged request (rounded down to 64 / 32) and one wider than d (clamped to 128)
+WIDE_TILES = [(a, b) for a in (32, 64, 128) for b in (32, 64, 128)] + [(100, 48), (512, 512)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
