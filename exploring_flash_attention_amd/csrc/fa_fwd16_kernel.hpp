@@ -385,11 +385,15 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
     for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[qb][ks]));
-    // the first QK^T needs Q (waited above) and K(0) only: V(0) and K(1), the 2 * DPW pieces
-    // issued after it, stay in flight; the barrier after the row max drains them (A/B round 4,
-    // profiles/r04/ab_early_qk.txt: C3 +0.2 / +0.6 %, C4 +0.1 %, L = 2048 +0.3 %, bitwise equal)
+    // the first QK^T needs Q (waited above) and K(0) only: V(0) and K(1) -- the DPW pieces each
+    // issued after it; no K(1) for a single tile -- stay in flight; the barrier after the row max
+    // drains them (A/B round 4, profiles/r04/ab_early_qk.txt: C3 +0.2 / +0.6 %, C4 +0.1 %,
+    // L = 2048 +0.3 %, bitwise equal)
     static_assert(2 * DPW < 16, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPW) : "memory");
+    if (ntiles > 1)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPW) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(DPW) : "memory");
     FA_STAMP(1);
     f32x4 sa[NKB][NQB], sb[NKB][NQB];
     float mx[NQB];
