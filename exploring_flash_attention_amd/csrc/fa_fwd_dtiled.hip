@@ -49,7 +49,10 @@ constexpr int kDtSlotB = kDtBK * kDtMaxChunk * 2;
 #define FA_DT512_WPS 2  // waves per SIMD at d = 512 (2: 252 VGPRs, no scratch; 1: 8 ring slots)
 #endif
 constexpr int dt_wps(int d) { return d <= 384 ? FA_DT384_WPS : FA_DT512_WPS; }
-constexpr int dt_slots(int d) { return dt_wps(d) == 2 ? 4 : 8; }
+#ifndef FA_DT_SLOTS2
+#define FA_DT_SLOTS2 4  // ring slots at two workgroups per CU
+#endif
+constexpr int dt_slots(int d) { return dt_wps(d) == 2 ? FA_DT_SLOTS2 : 8; }
 
 int dtiled_rows_per_block() { return kDtRows; }
 int dtiled_lds_bytes(int d) { return dt_slots(d) * kDtSlotB; }
@@ -175,9 +178,28 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     // the stream fewer, and the wait drains), every wave is done with chunk gi-1, whose slot
     // the chunk gi + NSLOT - 1 then refills
     int cslot = 0;
+#ifndef FA_DT_GROUP
+#define FA_DT_GROUP 1
+#endif
+    // GRP = 2: chunks made readable in pairs -- one barrier per two chunks, the ring holding the
+    // pair in use and the next pair in flight
+    constexpr int GRP = (FA_DT_GROUP == 2 && per_tile % 2 == 0 && NSLOT == 4) ? 2 : 1;
     auto advance = [&](auto pos_c, int t) {
         constexpr int pos = decltype(pos_c)::value;
         const int gi = t * per_tile + pos;
+        if constexpr (GRP == 2) {
+            if constexpr (pos % 2 == 0) {
+                wait_vm<0>();  // this pair is all that is in flight
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (gi + 2 < total)
+                    issue(std::integral_constant<int, (pos + 2) % per_tile>{}, t + (pos + 2) / per_tile, (cslot + 2) & 3);
+                if (gi + 3 < total)
+                    issue(std::integral_constant<int, (pos + 3) % per_tile>{}, t + (pos + 3) / per_tile, (cslot + 3) & 3);
+            }
+            const char* const slot = smem + cslot * kDtSlotB;
+            cslot = (cslot + 1) & 3;
+            return slot;
+        }
         if (gi + NSLOT - 1 <= total)
             wait_vm<S::after(pos)>();
         else
@@ -250,7 +272,7 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     issue(std::integral_constant<int, 0>{}, 0, 0);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));
-    static_for<NSLOT - 2>([&](auto i_c) {
+    static_for<(GRP == 2 ? 3 : NSLOT) - 2>([&](auto i_c) {  // chunks 1 .. (pair 0 only when paired)
         constexpr int i = decltype(i_c)::value + 1;
         issue(std::integral_constant<int, i>{}, 0, i);
     });
