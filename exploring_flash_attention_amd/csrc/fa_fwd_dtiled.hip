@@ -31,6 +31,7 @@
 //     retires the previous chunk's slot;
 //   * registers: d = 384 and 512 both fit 256 (two workgroups per CU: 224 / 252 VGPRs).
 #include "fa_device.hpp"
+#include "fa_dtiled_stream.hpp"
 
 namespace fa {
 
@@ -79,21 +80,6 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t rs, const char*
 }
 #pragma clang diagnostic pop
 
-// The chunk stream of one (d, d_tile_qk, d_tile_v): per 64-key tile NQC K chunks of DQ columns
-// then NVC V chunks of DV columns, each chunk 1 KiB pieces, DQ / 32 (DV / 32) per wave.
-template <int D, int DQ, int DV, int NSLOT>
-struct DtStream {
-    static constexpr int NQC = D / DQ, NVC = D / DV, PER_TILE = NQC + NVC;
-    static constexpr int KPW = DQ / 32, VPW = DV / 32;
-    static constexpr int pieces(int pos) { return pos < NQC ? KPW : VPW; }
-    // pieces of the NSLOT - 2 chunks issued after the chunk at position pos (steady state)
-    static constexpr int after(int pos) {
-        int n = 0;
-        for (int i = 1; i <= NSLOT - 2; ++i) n += pieces((pos + i) % PER_TILE);
-        return n;
-    }
-};
-
 template <typename T, int D, int DQ, int DV>
 __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     using M = Mma<T>;
@@ -119,7 +105,10 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
 
     // chunk geometry (effective tiles: 32, 64 or 128 columns, dividing D; one instantiation
     // per pair, so every chunk boundary and every DMA count below is a compile-time constant)
-    using S = DtStream<D, DQ, DV, NSLOT>;
+#ifndef FA_DT_GROUP
+#define FA_DT_GROUP 1  // 2: chunks made readable in pairs, one barrier per pair (4 slots)
+#endif
+    using S = DtStream<D, DQ, DV, NSLOT, FA_DT_GROUP>;
     constexpr int nqc = S::NQC, per_tile = S::PER_TILE;
     constexpr int kpc = DQ / 32;          // QK^T k-steps per K chunk
     constexpr int bpc = DV / 16;          // O^T column blocks per V chunk
@@ -174,43 +163,26 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
         for (int p = 0; p < pw; ++p) dma16_asm(rs, slot + (wid * pw + p) * 1024, isk ? ksrc[p] : vsrc[p]);
     };
     // chunk gi = t * per_tile + pos (the next to consume) becomes readable: its pieces landed
-    // (in the steady state exactly S::after(pos) pieces were issued after it; near the end of
-    // the stream fewer, and the wait drains), every wave is done with chunk gi-1, whose slot
-    // the chunk gi + NSLOT - 1 then refills
+    // (the protocol of fa_dtiled_stream.hpp: a counted wait, a barrier after which every wave is
+    // done with the slots being refilled, the next chunk(s) issued into them)
     int cslot = 0;
-#ifndef FA_DT_GROUP
-#define FA_DT_GROUP 1
-#endif
-    // GRP = 2: chunks made readable in pairs -- one barrier per two chunks, the ring holding the
-    // pair in use and the next pair in flight
-    constexpr int GRP = (FA_DT_GROUP == 2 && per_tile % 2 == 0 && NSLOT == 4) ? 2 : 1;
     auto advance = [&](auto pos_c, int t) {
         constexpr int pos = decltype(pos_c)::value;
-        const int gi = t * per_tile + pos;
-        if constexpr (GRP == 2) {
-            if constexpr (pos % 2 == 0) {
-                wait_vm<0>();  // this pair is all that is in flight
-                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                if (gi + 2 < total)
-                    issue(std::integral_constant<int, (pos + 2) % per_tile>{}, t + (pos + 2) / per_tile, (cslot + 2) & 3);
-                if (gi + 3 < total)
-                    issue(std::integral_constant<int, (pos + 3) % per_tile>{}, t + (pos + 3) / per_tile, (cslot + 3) & 3);
-            }
-            const char* const slot = smem + cslot * kDtSlotB;
-            cslot = (cslot + 1) & 3;
-            return slot;
-        }
-        if (gi + NSLOT - 1 <= total)
-            wait_vm<S::after(pos)>();
-        else
-            wait_vm<0>();
-        // the barrier as inline asm with a memory clobber: no memory operation (the next DMA
-        // into the retired slot above all) may be moved across it, and no drain is implied
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (gi + NSLOT - 1 < total) {
-            constexpr int npos = (pos + NSLOT - 1) % per_tile;
-            issue(std::integral_constant<int, npos>{}, t + (pos + NSLOT - 1) / per_tile,
-                  cslot == 0 ? NSLOT - 1 : cslot - 1);
+        if constexpr (S::syncs(pos)) {
+            const int gi = t * per_tile + pos;
+            if (S::steady(gi, total))
+                wait_vm<S::after(pos)>();
+            else
+                wait_vm<0>();
+            // the barrier as inline asm with a memory clobber: no memory operation (the next DMA
+            // into a retired slot above all) may be moved across it, and no drain is implied
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            static_for<S::GRP>([&](auto j_c) {
+                constexpr int j = decltype(j_c)::value, np = pos + S::LEAD + j;
+                if (gi + S::LEAD + j < total)
+                    issue(std::integral_constant<int, np % per_tile>{}, t + np / per_tile,
+                          S::slot_after(cslot, S::LEAD + j));
+            });
         }
         const char* const slot = smem + cslot * kDtSlotB;
         cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
@@ -263,16 +235,15 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
         }
     };
 
-    // The first NSLOT - 1 chunks (positions and tiles static; total >= per_tile >= NSLOT - 1):
-    // chunk 0, then a fence that has the compiler wait for Q (vmcnt(0): it counts only the Q
-    // loads, and chunk 0 went out before them), then the rest in flight.  Without the fence the
-    // compiler places a wait for Q before each k-step's first MFMA, inside the loop, where its
-    // counts would drain the ring.
-    static_assert(NSLOT - 1 <= per_tile, "the first ring fill lies within tile 0");
+    // The first S::FILL chunks (positions and tiles static; total >= per_tile >= FILL): chunk 0,
+    // then a fence that has the compiler wait for Q (vmcnt(0): it counts only the Q loads, and
+    // chunk 0 went out before them), then the rest in flight.  Without the fence the compiler
+    // places a wait for Q before each k-step's first MFMA, inside the loop, where its counts
+    // would drain the ring.
     issue(std::integral_constant<int, 0>{}, 0, 0);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));
-    static_for<(GRP == 2 ? 3 : NSLOT) - 2>([&](auto i_c) {  // chunks 1 .. (pair 0 only when paired)
+    static_for<S::FILL - 1>([&](auto i_c) {
         constexpr int i = decltype(i_c)::value + 1;
         issue(std::integral_constant<int, i>{}, 0, i);
     });
