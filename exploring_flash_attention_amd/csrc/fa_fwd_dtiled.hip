@@ -25,7 +25,7 @@
 //   * a query's 64 scores of a tile sit in 4 lanes (n, n+16, n+32, n+48): row max by two
 //     permlane swaps, row sums by a 16x16x32 MFMA with A = ones (as fa_fwd16_kernel.hpp);
 //   * LDS: a ring of 16 KiB chunk images (the swizzled 8-row x 32-column subtile image of
-//     fa_device.hpp, row = 2 * chunk bytes; 4 slots), filled by LDS-DMA
+//     fa_device.hpp, row = 2 * chunk bytes; 3 slots at d = 384, 4 at d = 512), filled by LDS-DMA
 //     NSLOT-1 chunks ahead of use: the chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one
 //     raw barrier per chunk, the DMA of the next chunk issued right after the barrier that
 //     retires the previous chunk's slot;
@@ -40,9 +40,9 @@ constexpr int kDtRows = 16 * kDtWaves;  // query rows per workgroup
 constexpr int kDtBK = 64;               // keys per tile
 constexpr int kDtMaxChunk = 128;        // columns per LDS chunk at most
 constexpr int kDtSlotB = kDtBK * kDtMaxChunk * 2;
-// ring slots: two workgroups per CU (one wave per SIMD each), 4 x 16 KiB each; one workgroup per
-// CU would take 8 slots -- 7 chunks in flight -- and measured slower (d = 512: 903 vs 672 us at
-// B32 H8 L1024, profiles/r04/ab_dtiled_g.log)
+// ring slots: two workgroups per CU (one wave per SIMD each), 3 / 4 x 16 KiB each; one workgroup
+// per CU would take 8 slots -- 7 chunks in flight -- and measured slower (d = 512: 903 vs 672 us
+// at B32 H8 L1024, profiles/r04/ab_dtiled_g.log)
 #ifndef FA_DT384_WPS
 #define FA_DT384_WPS 2  // waves per SIMD at d = 384 (2: two workgroups per CU)
 #endif
@@ -50,10 +50,14 @@ constexpr int kDtSlotB = kDtBK * kDtMaxChunk * 2;
 #define FA_DT512_WPS 2  // waves per SIMD at d = 512 (2: 252 VGPRs, no scratch; 1: 8 ring slots)
 #endif
 constexpr int dt_wps(int d) { return d <= 384 ? FA_DT384_WPS : FA_DT512_WPS; }
+// ring slots at two workgroups per CU: 3 at d = 384, 4 at d = 512 (A/B, profiles/r04/
+// ab_dtiled_ring.txt: d = 384 3 / 4 / 5 slots 505 / 519 / 521 us, d = 512 690 / 668 / 682 us)
 #ifndef FA_DT_SLOTS2
-#define FA_DT_SLOTS2 4  // ring slots at two workgroups per CU
+#define FA_DT_SLOTS2 0  // 0: the measured choice above; n: n slots at both head dims (A/B builds)
 #endif
-constexpr int dt_slots(int d) { return dt_wps(d) == 2 ? FA_DT_SLOTS2 : 8; }
+constexpr int dt_slots(int d) {
+    return dt_wps(d) == 2 ? (FA_DT_SLOTS2 > 0 ? FA_DT_SLOTS2 : d <= 384 ? 3 : 4) : 8;
+}
 
 int dtiled_rows_per_block() { return kDtRows; }
 int dtiled_lds_bytes(int d) { return dt_slots(d) * kDtSlotB; }

@@ -13,5 +13,5 @@ int fwd64_keys_per_tile() { return 16; }
 __attribute__((weak)) hipError_t launch_fwd_dtiled(Elem, int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
 hipError_t launch_fwd64_dtiled(int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
 __attribute__((weak)) int dtiled_rows_per_block() { return 64; }
-__attribute__((weak)) int dtiled_lds_bytes(int d) { return (d <= 384 ? 4 : 8) * 16384; }
+__attribute__((weak)) int dtiled_lds_bytes(int d) { return (d <= 384 ? 3 : 4) * 16384; }
 }  // namespace fa
