@@ -308,7 +308,7 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
     return FA_OK;
 }
 
-// Work order of the fused split launch (FwdArgs::split_fastest): split fastest when the whole
+// Work order of the fused split launch (FwdArgs::tile_group): split fastest when the whole
 // grid is resident at once (at most two workgroups per CU) and a query tile has at least 4
 // partials, query tile fastest otherwise.
 // Measured (round 4, A/B in one process, profiles/r04/ab_split_order.log; outputs bitwise
@@ -320,11 +320,19 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
 #ifndef FA_SPLIT_ORDER_RULE
 #define FA_SPLIT_ORDER_RULE 2  // 0: query tile fastest always; 1: split fastest always; 2: the rule
 #endif
-int split_fastest(int64_t nblk, int ns) {
-    if (FA_SPLIT_ORDER_RULE != 2) return FA_SPLIT_ORDER_RULE == 1;
+// At >= 8 partials per tile (the reference's one-block-per-workgroup layout) groups of 4 query
+// tiles with their splits consecutive: C4 at blocks_per_workgroup = 1 3448 -> 3334 us (groups
+// of 8: 3361; profiles/r04/ab_tile_group.txt, outputs bitwise equal) -- a group's partials are
+// combined while still in L2, and each key block's K / V still serves 4 tiles.
+#ifndef FA_TILE_GROUP
+#define FA_TILE_GROUP 4  // 0: off
+#endif
+int tile_group(int64_t nblk, int ns, int nqt) {
+    if (FA_TILE_GROUP > 0 && ns >= 8 && nqt % FA_TILE_GROUP == 0) return FA_TILE_GROUP;
+    if (FA_SPLIT_ORDER_RULE != 2) return FA_SPLIT_ORDER_RULE == 1 ? 1 : 0;
     // (B1 H1 L16384, 2 partials: equal time either way, but split fastest puts both halves of
     // the keys on every XCD -- 93 MB of L2 egress per launch against 64 MB (profiles/r04))
-    return ns >= 4 && nblk <= 2 * (int64_t)device_cus();
+    return ns >= 4 && nblk <= 2 * (int64_t)device_cus() ? 1 : 0;
 }
 
 // workspace bytes for a plan (the grid bound checked too)
@@ -532,7 +540,7 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     a.o = workspace;
     a.lse = (float*)((char*)workspace + w.lse_off);
     a.esc = (float*)((char*)workspace + w.esc_off);
-    a.split_fastest = split_fastest((int64_t)a.nqt * ns * BH, ns);
+    a.tile_group = tile_group((int64_t)a.nqt * ns * BH, ns, a.nqt);
     a.counters = (unsigned*)((char*)workspace + w.cnt_off);
     a.o_final = o;
     // the kernel leaves every counter at zero; clearing them here makes a call that follows

@@ -75,24 +75,35 @@ struct FwdArgs {
     int64_t q_stride[3], k_stride[3], o_stride[3];
     // d-tiled kernels (d = 384 / 512): effective column chunks of K and V (32, 64 or 128)
     int d_tile_qk, d_tile_v;
-    // fused split mode: the order of the work items in the (remapped) block index -- 0: query
-    // tile fastest (the 32 tiles of one key block share its K / V in L2), 1: split fastest (the
-    // splits of one query tile run together: Q re-read from L2, partials combined while hot)
-    int split_fastest;
+    // fused split mode: the order of the work items in the (remapped) block index, as groups of
+    // tile_group query tiles (dividing nqt) whose splits are consecutive -- 0 or nqt: query tile
+    // fastest (the tiles of one key block share its K / V in L2), 1: split fastest (the splits
+    // of one query tile run together: Q re-read from L2, partials combined while hot), between:
+    // both, for a group of tiles
+    int tile_group;
 };
 
 // (query tile, split, b*h) of work item w (after xcd_remap)
 __device__ __forceinline__ void decode_item(const FwdArgs& a, int w, int& qt, int& split, int64_t& bh) {
-    if (a.split_fastest) {
-        split = w % a.nsplit;
-        const int rest = w / a.nsplit;
-        qt = rest % a.nqt;
-        bh = rest / a.nqt;
-    } else {
+    const int G = a.tile_group;
+    if (G <= 0 || G >= a.nqt) {  // (b*h, split, query tile)
         qt = w % a.nqt;
         const int rest = w / a.nqt;
         split = rest % a.nsplit;
         bh = rest / a.nsplit;
+    } else if (G == 1) {  // (b*h, query tile, split)
+        split = w % a.nsplit;
+        const int rest = w / a.nsplit;
+        qt = rest % a.nqt;
+        bh = rest / a.nqt;
+    } else {  // (b*h, tile group, split, tile in group)
+        const int qi = w % G;
+        int rest = w / G;
+        split = rest % a.nsplit;
+        rest /= a.nsplit;
+        const int ng = a.nqt / G;
+        qt = (rest % ng) * G + qi;
+        bh = rest / ng;
     }
 }
 

@@ -60,7 +60,7 @@ class Alloc:
 
 
 def replay(args, allocs, kernel16, strided=None, qstr=None, mode="final", pt_bytes=2, scaled=False,
-           flat_decode=False, split_fastest=False):
+           flat_decode=False, tile_group=0):
     """Replay one launch.  args: the FwdArgs fields the kernels read; allocs: q, k, v, o (and
     for fused: ws_o, ws_lse, ws_esc, counters, o_final)."""
     BH, Lq, Lk, D = args["BH"], args["Lq"], args["Lk"], args["D"]
@@ -72,9 +72,15 @@ def replay(args, allocs, kernel16, strided=None, qstr=None, mode="final", pt_byt
     assert np.array_equal(np.sort(w), b), "xcd_remap is not a bijection onto the grid"
     qt, rest = w % nqt, w // nqt
     split, bh = rest % nsplit, rest // nsplit
-    if split_fastest:  # fa_internal.hpp decode_item, FwdArgs::split_fastest
+    if tile_group == 1:  # fa_internal.hpp decode_item, FwdArgs::tile_group
         split, rest = w % nsplit, w // nsplit
         qt, bh = rest % nqt, rest // nqt
+    elif 1 < tile_group < nqt:
+        assert nqt % tile_group == 0
+        qi, rest = w % tile_group, w // tile_group
+        split, rest = rest % nsplit, rest // nsplit
+        ng = nqt // tile_group
+        qt, bh = (rest % ng) * tile_group + qi, rest // ng
     if flat_decode:  # (test_replay_catches_a_bad_decode: the split index ignored)
         split, bh = np.zeros_like(rest), rest
     assert bh.max() < BH and bh.min() >= 0, f"b*h decoded up to {int(bh.max())} of {BH}"
@@ -183,7 +189,7 @@ def test_c3_decode_of_the_aborting_commit_equals_the_fixed_one():
     assert np.array_equal(old_bh, new_bh) and old_bh.max() == 255
 
 
-@pytest.mark.parametrize("order", ["qtile-fastest", "split-fastest"])
+@pytest.mark.parametrize("order", ["qtile-fastest", "split-fastest", "tile-group-4"])
 @pytest.mark.parametrize("group", [0, 1, 4, 16], ids=["auto", "1-per-wg", "4-per-wg", "16-per-wg"])
 @pytest.mark.parametrize("B,H,L", [(32, 8, 4096), (1, 1, 16384), (1, 2, 4096), (2, 2, 1000)],
                          ids=["C4", "b1h1-l16k", "b1h2-l4k", "tail"])
@@ -206,7 +212,8 @@ def test_fused_split_in_bounds(B, H, L, group, order):
     allocs.update(ws_o=Alloc("ws partials", nbytes), ws_lse=Alloc("ws lse", nbytes - lse_off),
                   ws_esc=Alloc("ws esc", nbytes - esc_off), counters=Alloc("ws counters", nbytes - cnt_off),
                   o_final=_tensor("o", B, H, L, d))
-    replay(a, allocs, L % 64 == 0, mode="fused", scaled=True, split_fastest=order == "split-fastest")
+    replay(a, allocs, L % 64 == 0, mode="fused", scaled=True,
+           tile_group={"qtile-fastest": 0, "split-fastest": 1, "tile-group-4": 4}[order])
 
 
 @pytest.mark.parametrize("W", [2, 8])
