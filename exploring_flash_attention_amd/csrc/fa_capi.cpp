@@ -323,16 +323,22 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
 // At >= 8 partials per tile (the reference's one-block-per-workgroup layout) groups of 4 query
 // tiles with their splits consecutive: C4 at blocks_per_workgroup = 1 3448 -> 3334 us (groups
 // of 8: 3361; profiles/r04/ab_tile_group.txt, outputs bitwise equal) -- a group's partials are
-// combined while still in L2, and each key block's K / V still serves 4 tiles.
+// combined while still in L2, and each key block's K / V still serves 4 tiles.  Groups of 2
+// lost 9 % there; at 4 partials per tile the groups measured +0.9 % (C4, 4 blocks per
+// workgroup) and -1.4 % (B2 H2 L16384) and stay off (profiles/r04/ab_tile_group_2.txt).
 #ifndef FA_TILE_GROUP
 #define FA_TILE_GROUP 4  // 0: off
 #endif
+#ifndef FA_TG_MIN
+#define FA_TG_MIN 8  // partials per tile from which queued grids take the tile groups
+#endif
 int tile_group(int64_t nblk, int ns, int nqt) {
-    if (FA_TILE_GROUP > 0 && ns >= 8 && nqt % FA_TILE_GROUP == 0) return FA_TILE_GROUP;
     if (FA_SPLIT_ORDER_RULE != 2) return FA_SPLIT_ORDER_RULE == 1 ? 1 : 0;
     // (B1 H1 L16384, 2 partials: equal time either way, but split fastest puts both halves of
     // the keys on every XCD -- 93 MB of L2 egress per launch against 64 MB (profiles/r04))
-    return ns >= 4 && nblk <= 2 * (int64_t)device_cus() ? 1 : 0;
+    if (ns >= 4 && nblk <= 2 * (int64_t)device_cus()) return 1;
+    if (FA_TILE_GROUP > 1 && ns >= FA_TG_MIN && nqt % FA_TILE_GROUP == 0) return FA_TILE_GROUP;
+    return 0;
 }
 
 // workspace bytes for a plan (the grid bound checked too)
