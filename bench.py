@@ -44,6 +44,38 @@ def flops(B, H, L, d, Lk=None):
     return 4.0 * B * H * L * (L if Lk is None else Lk) * d
 
 
+PROBE_LIB = os.path.join(ROOT, "exploring_flash_attention_amd", "_lib", "libfa_probe.so")
+
+
+def measured_ceiling(d):
+    """The MFMA rate this box sustains on random operands, on the shape the headline kernel
+    issues (d = 128: v_mfma_f32_16x16x32_bf16; other head dims: 32x32x16), measured live with
+    csrc/fa_probe.hip (4 accumulation chains per wave, 2 waves per SIMD, nothing else in the
+    loop; ~0.7 s).  The operand values set the MFMA array's power and so the clock the chip
+    holds (DESIGN.md section 5), which puts this ceiling far below the 2.5 PF datasheet figure;
+    roofline.frac stays against the datasheet, frac_of_measured is against this."""
+    import ctypes
+    shape = 1 if d == 128 else 0
+    names = {0: "v_mfma_f32_32x32x16_bf16", 1: "v_mfma_f32_16x16x32_bf16"}
+    try:
+        lib = ctypes.CDLL(PROBE_LIB)
+    except OSError as exc:
+        return {"error": f"libfa_probe.so not loadable: {exc}"[:200]}
+    lib.fa_probe_mfma_ceiling.argtypes = [ctypes.c_int] * 6 + [ctypes.POINTER(ctypes.c_double)]
+    res = {"shape": names[shape], "waves_per_simd": 2}
+    out = (ctypes.c_double * 3)()
+    iters = 2000 if shape == 1 else 1000  # ~50 ms per launch
+    # pattern 2: A repeated in pairs (the kernel's order: one K fragment / V^T operand feeds the
+    # wave's two query blocks); pattern 1: a new (A, B) pair every MFMA
+    for pat, key in ((2, "random_a_pairs"), (1, "random")):
+        rc = lib.fa_probe_mfma_ceiling(shape, pat, 2, iters, 5, 10, out)
+        if rc != 0:
+            return {"error": f"fa_probe_mfma_ceiling returned {rc}"}
+        res[key] = {"tflops": round(out[0], 1), "held_clock_mhz": round(out[1])}
+    res["tflops"] = res["random_a_pairs"]["tflops"]
+    return res
+
+
 # ------------------------------------------------------------------------------------
 # CPU baseline (oracle restatement of numpy_gpu_like_opt2.py), run BEFORE any GPU init
 # ------------------------------------------------------------------------------------
@@ -529,6 +561,7 @@ def main():
         torch.cuda.empty_cache()
 
     check = None
+    ceiling = None
     t_warm = 0.0
     if args.mode == "heads":
         q, k, v = _make_inputs(torch, dev, B, H, L, d, seed=1234 + rank)
@@ -554,6 +587,7 @@ def main():
         # untimed steps and exactly --steps timed ones.
         t_warm = clock_settle(torch, step, args.clock_warmup)
         wall, ev_ms = time_step(torch, step, args.steps, args.warmup, barrier)
+        ceiling = measured_ceiling(d) if rank == 0 else None  # after the timed window
         work = flops(B, H, L, d)
         workload = ("FA-v1 fused / tiled-d forward (one kernel)" if cfg["variant"] == "v1"
                     else "FA-v2 split-KV forward")
@@ -607,6 +641,11 @@ def main():
                          "kernel": kernel, "kernel_ms": round(avg_ms, 5)},
             "cpu_baseline": cpu,
         }
+        if ceiling is not None:
+            rf = line["roofline"]
+            rf["ceiling_measured"] = ceiling.get("tflops")
+            rf["frac_of_measured"] = (round(achieved / ceiling["tflops"], 4) if ceiling.get("tflops") else None)
+            rf["ceiling_source"] = ceiling
         if check is not None:
             line["check"] = check
         line["clock_warmup_s"] = round(t_warm, 3)

@@ -4,6 +4,11 @@
 #define FA_FWD_MAIN_TU
 #include "fa_fwd_kernel.hpp"
 #include "fa_fwd16_kernel.hpp"
+#include "fa_fwd16_chain.hpp"
+
+#ifndef FA_CHAIN
+#define FA_CHAIN 1  // d = 128 final mode: the chained persistent grid (fa_fwd16_chain.hpp)
+#endif
 
 
 namespace fa {
@@ -17,6 +22,17 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     // d = 128 without a key tail: the 16x16x32 kernel (fa_fwd16_kernel.hpp; C3 +5 %, C4 +3.4 %,
     // the C5 partial pass +9 % over this file's 32x32x16 kernel)
     if constexpr (D == 128) {
+        if constexpr (MODE == kFinal && std::is_same_v<T, PT> && FA_CHAIN) {
+            // whole query-tile chains: an even number of 64-key tiles and at least one query
+            // tile per workgroup of a 2-per-CU grid
+            const int64_t grid = 2 * (int64_t)device_cus() / 8 * 8;
+            if (a.Lk % 128 == 0 && a.Lk >= 384 && a.Lq % kBQ == 0 && a.nsplit == 1 && nblk >= grid && grid >= 8 &&
+                nblk < (int64_t)1 << 31) {
+                hipLaunchKernelGGL((fa_fwd16_chain_kernel<T>), dim3((unsigned)grid), dim3(kThreads), lds, s, a,
+                                   (int)nblk);
+                return hipGetLastError();
+            }
+        }
         if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {  // no key tail in any split
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();

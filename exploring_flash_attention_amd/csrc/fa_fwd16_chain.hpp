@@ -1,0 +1,473 @@
+// fa_fwd16_chain.hpp -- the d = 128 final-mode forward as a persistent grid whose workgroups run
+// a fixed list of query tiles back to back with no seam between them (round 5).
+//   <- flash_attention_kernel    flash_attention_v1/CUDA/flash_attention_v1.h:161
+//   <- flash_attention_kernel (tiled-d) flash_attention_v1_tiled_d/CUDA/flash_attention_v1.h:230
+//
+// Why: in the one-shot grid (fa_fwd16_kernel.hpp) every 128-row query tile is a workgroup that
+// pays a prologue (Q, K0, V0, K1 landing: 4.6 k cycles), a first QK^T outside the software
+// pipeline (1.7 k) and an epilogue (2.6 k + 1 k of store retirement) -- 20 % of its life at C3
+// (B32 H8 L1024: 16 KV steps per tile), covered only in part by the CU's other workgroup
+// (DESIGN.md section 5, round 4 stamps).  Here the KV step stream runs across tiles: the step
+// that finishes tile i's P.V also computes QK^T(0) of tile i+1 -- its K(0), K(1), V(0) were
+// DMA'd into the ring by the two preceding steps exactly as within a tile, and its Q^T was
+// loaded into the (then dead) Q registers during the P.V half of the step before -- so the
+// only work between two tiles is tile i's O normalisation and stores.
+//
+// Schedule: a grid of exactly 2 workgroups per CU (one wave per SIMD each, as the one-shot
+// kernel); workgroup b serves XCD group x = b % 8 (blocks b and b+8 share an XCD, observed
+// dispatch -- speed only) and takes the group's items l, l + G/8, l + 2G/8, ... (l = b / 8), of
+// the contiguous item range xcd_remap gives the group: at any time an XCD runs consecutive
+// items, i.e. all query tiles of a few heads, which share their K / V in that XCD's L2.
+// A persistent grid loses the one-shot grid's alternating age priority (a replacement
+// workgroup is younger than its CU partner, so the older one wins VALU-issue arbitration,
+// then the other way round); with fixed partners the older would keep winning (round 2: end
+// times 1543-2072 us at C4).  FA_CHAIN_TAP: each wave's issue priority alternates with the
+// 100 MHz real-time clock, opposite phase for the CU's two workgroups (TG_ID parity), so
+// each holds priority half of the time whatever their ages.
+//
+// Requirements (checked by the launcher): contiguous [B, H, L, d], d = 128, Lk a multiple of
+// 128 (an even number of 64-key tiles, so every tile starts on ring parity 0), at least as
+// many query tiles as workgroups.  Everything else is fa_fwd16_kernel.hpp's step, unchanged.
+#pragma once
+#include "fa_fwd16_kernel.hpp"
+
+#ifndef FA_CHAIN_QPF
+#define FA_CHAIN_QPF 4  // the next tile's Q is pulled into L2 this many steps before the seam (0: off)
+#endif
+#ifndef FA_CHAIN_TAP
+#define FA_CHAIN_TAP 1  // time-alternating issue priority between the CU's two workgroups
+#endif
+#ifndef FA_CHAIN_TAP_SHIFT
+#define FA_CHAIN_TAP_SHIFT 9  // priority period 2^shift x 10 ns (9: 5.12 us)
+#endif
+
+namespace fa {
+
+template <typename T>
+__global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, int nitems) {
+    using M = Mma<T>;
+    using v8 = typename M::v8;
+    constexpr int D = 128;
+    constexpr int ROWB = D * 2;
+    constexpr int kBK = 64;
+    constexpr int TILEB = kBK * ROWB;
+    constexpr int NKS = D / 32;
+    constexpr int NKB = kBK / 16;
+    constexpr int NQB = 2;
+    constexpr int NDB = D / 16;
+    constexpr int NKK = kBK / 32;
+    constexpr float kThr = 4.f;
+    constexpr int KA = 3, VA = 2;
+    constexpr int EXPA = 28;
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* const kring = smem;
+    char* const vring = smem + 2 * TILEB;
+
+    // this workgroup's items: group x = blockIdx % 8 owns xcd_remap's contiguous range
+    const int nl = gridDim.x >> 3, x = blockIdx.x & 7, l = blockIdx.x >> 3;
+    const int iq = nitems >> 3, ir = nitems & 7;
+    const int gstart = x < ir ? x * (iq + 1) : ir * (iq + 1) + (x - ir) * iq;
+    const int gcnt = iq + (x < ir ? 1 : 0);
+    const int nmine = l < gcnt ? (gcnt - l + nl - 1) / nl : 0;
+    if (nmine == 0) return;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n16 = lane & 15, g = lane >> 4;
+    const int ntiles = (int)(a.Lk / kBK);
+#if FA_CHAIN_TAP
+    const unsigned tgp = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 16) & 1;  // HW_ID.TG_ID parity
+#endif
+
+    // per-item addressing: (query tile, b*h) of item j of this workgroup
+    struct Item {
+        const unsigned short* k;
+        const unsigned short* v;
+        const unsigned short* q;  // first row of the query tile
+        int64_t o_row0;           // element offset of the tile's first O row
+        int64_t q_rows;
+    };
+    // (every field wave-uniform: readfirstlane keeps the loop-carried item in SGPRs -- a
+    // descriptor the compiler cannot prove uniform becomes a waterfall loop around each DMA)
+    auto uni = [](const unsigned short* p) {
+        const uint64_t u = (uint64_t)(size_t)p;
+        const uint64_t lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)u);
+        const uint64_t hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+        return (const unsigned short*)(size_t)(lo | (hi << 32));
+    };
+    auto item = [&](int j) {
+        const int w = __builtin_amdgcn_readfirstlane(gstart + l + nl * j);
+        const int qt = w % a.nqt;
+        const int64_t bh = w / a.nqt;
+        const int64_t q0 = (int64_t)qt * kBQ;
+        Item it;
+        it.k = uni((const unsigned short*)a.k + bh * a.Lk * D);
+        it.v = uni((const unsigned short*)a.v + bh * a.Lk * D);
+        it.q = uni((const unsigned short*)a.q + (bh * a.Lq + q0) * D);
+        it.o_row0 = (bh * a.Lq + q0) * D;
+        it.q_rows = a.Lq - q0 < kBQ ? a.Lq - q0 : kBQ;
+        return it;
+    };
+
+    const int pg = (0x2130 >> (4 * g)) & 3;
+    v8 qf[NQB][NKS];
+    auto load_q = [&](const Item& it) {
+        const __amdgpu_buffer_rsrc_t qrs = make_rsrc(uni(it.q), (it.q_rows - 1) * ROWB + ROWB);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks)
+                qf[qb][ks] = __builtin_bit_cast(
+                    v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, (wid * 32 + 16 * qb + n16) * ROWB + ks * 64 + pg * 16, 0, 0));
+    };
+
+    // LDS-DMA source offsets (fa_fwd16_kernel.hpp's dma_src[i]) as one VGPR + a scalar offset:
+    // piece i of a wave covers image bytes (4 * wid + i) KiB, i.e. row group 2 * wid + i / 2 and
+    // the upper 1 KiB (16-byte chunks 8..15) for odd i, so its source is piece 0's + 2048 * (i / 2)
+    // + 128 * (i & 1) -- one register fewer per piece in a kernel at the 256-register limit
+    constexpr int DPW = TILEB / 1024 / kWaves;
+    static_assert(DPW == 4 && ROWB == 256, "piece geometry");
+    int dma_src0;
+    {
+        const int b = wid * DPW * 1024 + lane * 16;
+        const int rg = b / (8 * ROWB), rem = b % (8 * ROWB);
+        const int row = 8 * rg + (rem % 512) / 64;
+        const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
+        dma_src0 = row * ROWB + ch * 16;
+    }
+    auto piece_soff = [](int i) { return 2048 * (i >> 1) + 128 * (i & 1); };
+    auto tile_rsrc = [&](const unsigned short* base, int t) {
+        return make_rsrc32(uni(base + (int64_t)t * (TILEB / 2)), TILEB);
+    };
+    auto dma_tile = [&](const unsigned short* base, char* slot, int t) {
+        const __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, t);
+#pragma unroll
+        for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src0, piece_soff(i));
+    };
+
+    const int rho = 8 * ((n16 >> 2) & 1) + 4 * (n16 >> 3) + (n16 & 3);
+    const unsigned kaddr = (unsigned)(size_t)kring + (rho >> 3) * (8 * ROWB) + 64 * (rho & 7) + 16 * (pg ^ ((rho >> 2) & 3));
+    const int r0 = 8 * (g & 1) + 4 * (g >> 1) + (n16 >> 2);
+    const int sw = (r0 >> 2) & 3, c0 = (n16 >> 1) & 1;
+    const unsigned vrow = (unsigned)(size_t)vring + (r0 >> 3) * (8 * ROWB) + 64 * (r0 & 7) + 8 * (n16 & 1);
+    const unsigned vb_e = vrow + 16 * (c0 ^ sw);
+    const unsigned vb_o = vrow + 16 * ((2 + c0) ^ sw);
+
+    f32x4 o[NDB][NQB];
+    f32x4 rs[NQB];
+    float m[NQB];
+    v8 ones;
+    {
+        constexpr unsigned kOne = std::is_same_v<T, __bf16> ? 0x3F80u : 0x3C00u;
+        ones = __builtin_bit_cast(v8, u32x4{kOne | (kOne << 16), kOne | (kOne << 16), kOne | (kOne << 16),
+                                            kOne | (kOne << 16)});
+    }
+    const float c = a.scale_log2;
+
+    auto kread_ = [](auto r_c, auto slot_c, u32x4 (&kf)[KA + 1], unsigned ka) {
+        constexpr int R = decltype(r_c)::value, KS = R / NKB, KB = R % NKB, SL = decltype(slot_c)::value;
+        constexpr int OFF = SL * TILEB + KB * 16 * ROWB + KS * 512;
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[R % (KA + 1)]) : "v"(ka), "i"(OFF) : "memory");
+    };
+    auto vread_ = [](auto p_c, auto slot_c, u32x2 (&vf)[VA + 1][2], unsigned ve, unsigned vo) {
+        constexpr int PP = decltype(p_c)::value, KK = PP / NDB, DB = PP % NDB, SL = decltype(slot_c)::value;
+        constexpr int OFF = SL * TILEB + KK * 32 * ROWB + 512 * (DB >> 1);
+        if constexpr (DB & 1) {
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][0]) : "v"(vo), "i"(OFF) : "memory");
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][1]) : "v"(vo), "i"(OFF + 16 * ROWB) : "memory");
+        } else {
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][0]) : "v"(ve), "i"(OFF) : "memory");
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vf[PP % (VA + 1)][1]) : "v"(ve), "i"(OFF + 16 * ROWB) : "memory");
+        }
+    };
+    auto lwait = [](auto n_c, u32x4& reg) {
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(reg) : "i"(decltype(n_c)::value) : "memory");
+    };
+    auto lwait2 = [](auto n_c, u32x2 (&reg)[2]) {
+        asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(reg[0]), "+v"(reg[1]) : "i"(decltype(n_c)::value) : "memory");
+    };
+    auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+
+    auto qk_all = [&](auto slot_c, f32x4 (&s)[NKB][NQB]) {
+        u32x4 kf[KA + 1];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int qb = 0; qb < NQB; ++qb) s[kb][qb] = f32x4{};
+        static_for<KA>([&](auto r_c) { kread_(r_c, slot_c, kf, kaddr); });
+        static_for<NKS * NKB>([&](auto s_c) {
+            constexpr int S = decltype(s_c)::value;
+            if constexpr (S + KA < NKS * NKB) kread_(std::integral_constant<int, S + KA>{}, slot_c, kf, kaddr);
+            constexpr int AFTER = (S + KA < NKS * NKB ? S + KA : NKS * NKB - 1) - S;
+            lwait(std::integral_constant<int, AFTER>{}, kf[S % (KA + 1)]);
+#pragma unroll
+            for (int qb = 0; qb < NQB; ++qb)
+                s[S % NKB][qb] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[qb][S / NKB], s[S % NKB][qb]);
+        });
+    };
+    auto chain_max = [](const f32x4 (&s)[NKB][NQB], auto ch_c, auto h_c, float& acc) {
+        constexpr int CH = decltype(ch_c)::value, H = decltype(h_c)::value;
+        constexpr int QB = CH / 2, KB = 2 * (CH % 2) + H;
+        if constexpr (H == 0)
+            acc = fmax_nc(fmax_nc(fmax_nc(s[KB][QB][0], s[KB][QB][1]), s[KB][QB][2]), s[KB][QB][3]);
+        else
+            acc = fmax_nc(fmax_nc(fmax_nc(fmax_nc(acc, s[KB][QB][0]), s[KB][QB][1]), s[KB][QB][2]), s[KB][QB][3]);
+    };
+    auto rowmax_all = [&](const f32x4 (&s)[NKB][NQB], float (&mx)[NQB]) {
+        float m4[4];
+        static_for<8>([&](auto i_c) {
+            constexpr int I = decltype(i_c)::value;
+            chain_max(s, std::integral_constant<int, I / 2>{}, std::integral_constant<int, I % 2>{}, m4[I / 2]);
+        });
+        quad_max2(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]), mx[0], mx[1]);
+        mx[0] *= c;
+        mx[1] *= c;
+    };
+
+#if FA_CHAIN_TAP
+    unsigned hi = tgp;  // this wave holds the higher issue priority (both phases) while hi == 1
+#endif
+    // O rows of the previous item, normalised and stored while the next item's first step runs
+    // (EPI): lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n]; dv blocks 2e and 2e+1 are
+    // paired by one v_permlane16_swap per dword into a 16-byte row store (fa_fwd16_kernel.hpp)
+    const int o_lane = (wid * 32 + n16) * ROWB + 2 * (16 * (g & 1) + 8 * (g >> 1));
+    float einv[NQB] = {0.f, 0.f};  // 1 / row sum of the item whose O is still in the registers
+    auto store_group = [&](auto g_c, __amdgpu_buffer_rsrc_t ors) {
+        constexpr int G = decltype(g_c)::value, QB = G / 4, E = G % 4;
+        const float inv = einv[QB];
+        const unsigned x0 = pack2<T>(o[2 * E][QB][0] * inv, o[2 * E][QB][1] * inv);
+        const unsigned x1 = pack2<T>(o[2 * E][QB][2] * inv, o[2 * E][QB][3] * inv);
+        const unsigned y0 = pack2<T>(o[2 * E + 1][QB][0] * inv, o[2 * E + 1][QB][1] * inv);
+        const unsigned y1 = pack2<T>(o[2 * E + 1][QB][2] * inv, o[2 * E + 1][QB][3] * inv);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{s0[0], s1[0], s0[1], s1[1]}, ors,
+                                               o_lane + QB * 16 * ROWB + E * 64, 0, 0);
+    };
+    auto o_rsrc = [&](const Item& it) { return make_rsrc(uni((const unsigned short*)a.o + it.o_row0), kBQ * ROWB); };
+
+    // One step of fa_fwd16_kernel.hpp (see there); what differs is only where the tiles come
+    // from: krs / vrs describe the K tile fetched now (t+2, possibly the next item's 0 or 1)
+    // and the V tile (t+1, possibly the next item's 0), and QK^T(t+1) reads whatever Q^T the
+    // registers hold -- the next item's during the last step of an item.  Flags: 1 MORE (a tile
+    // t+1 exists: QK^T, row max, V DMA), 4 DMAK (a K tile is fetched), 8 QNEXT (the next item's
+    // Q^T is loaded in phase B, after phase A's last read of the current one, and the closing
+    // barrier leaves those loads in flight), 16 QPF (the next item's Q is pulled toward L2),
+    // 32 EPI (step 0 of an item whose predecessor's O is still in the registers: phase A stores
+    // it, one 16-byte row store per even slot, and phase B's first P.V / row-sum MFMAs start
+    // from zero instead of accumulating).
+    auto step = [&](auto par_c, auto flags_c, f32x4 (&sc)[NKB][NQB], f32x4 (&sn)[NKB][NQB], float (&mx)[NQB],
+                    __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt,
+                    __amdgpu_buffer_rsrc_t ors) {
+        constexpr int P = decltype(par_c)::value;
+        constexpr int F = decltype(flags_c)::value;
+        constexpr bool MORE = F & 1;
+        constexpr bool DMAK = F & 4;
+        constexpr bool QNEXT = F & 8;
+        constexpr bool QPF = F & 16;
+        constexpr bool EPI = F & 32;
+        using SLN = std::integral_constant<int, 1 - P>;
+        using SLC = std::integral_constant<int, P>;
+        if (!EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
+#pragma unroll
+            for (int qb = 0; qb < NQB; ++qb) {
+                const float m_new = fmaxf(m[qb], mx[qb]);
+                const float alpha = __builtin_amdgcn_exp2f(m[qb] - m_new);
+                m[qb] = m_new;
+                rs[qb] *= alpha;
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
+            }
+        }
+#if FA_CHAIN_TAP
+        if (hi)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+#endif
+        const float nm0 = -m[0], nm1 = -m[1];
+        char* const kdst = kring + P * TILEB + wid * DPW * 1024;
+        char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
+        unsigned pf = 0;
+        if constexpr (QPF)  // one dword per 128-byte line of the next tile's Q (256 lines, 4 waves)
+            pf = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(uni(nxt.q), nxt.q_rows * ROWB), (wid * 64 + lane) * 128, 0, 0);
+
+        auto ex = [&](auto e_c) {
+            constexpr int E = decltype(e_c)::value, KK = E / 16, QB = (E / 8) & 1, KB = 2 * KK + ((E / 4) & 1), I = E & 3;
+            sc[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, QB ? nm1 : nm0));
+        };
+        u32x4 pbu[NKK][NQB];
+        auto cvt = [&](auto k_c) {
+            constexpr int K = decltype(k_c)::value, KK = K / 8, QB = (K / 4) & 1, J = K % 4;
+            constexpr int KB = 2 * KK + (J >> 1), I = 2 * (J & 1);
+            pbu[KK][QB][J] = pack2<T>(sc[KB][QB][I], sc[KB][QB][I + 1]);
+        };
+        auto dma = [&](auto i_c) {
+            constexpr int I = decltype(i_c)::value;
+            if constexpr (I < DPW) {
+                if constexpr (DMAK) dma16(krs, kdst + I * 1024, dma_src0, piece_soff(I));
+            } else if constexpr (MORE) {
+                dma16(vrs, vdst + (I - DPW) * 1024, dma_src0, piece_soff(I - DPW));
+            }
+        };
+
+        // ---- phase A: QK^T(t+1) || exponentials of t
+#if !FA_CHAIN_TAP
+        if constexpr (MORE) __builtin_amdgcn_s_setprio(1);
+#endif
+        u32x4 kf[KA + 1];
+        if constexpr (MORE) {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb) sn[kb][qb] = f32x4{};
+            static_for<KA>([&](auto r_c) { kread_(r_c, SLN{}, kf, kaddr); });
+        }
+        static_for<16>([&](auto s_c) {
+            constexpr int S = decltype(s_c)::value;
+            if constexpr (MORE) {
+                if constexpr (S + KA < 16) kread_(std::integral_constant<int, S + KA>{}, SLN{}, kf, kaddr);
+                constexpr int AFTER = (S + KA < 16 ? S + KA : 15) - S;
+                lwait(std::integral_constant<int, AFTER>{}, kf[S % (KA + 1)]);
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb)
+                    sn[S % NKB][qb] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[qb][S / NKB], sn[S % NKB][qb]);
+            }
+            constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;
+            static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
+            if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});
+            if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
+            if constexpr (EPI && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ors);
+            if constexpr (MORE) fence();
+        });
+
+        // ---- phase B: P.V(t) || exponentials of t (rest), row max of t+1
+#if !FA_CHAIN_TAP
+        __builtin_amdgcn_s_setprio(0);
+#endif
+        if constexpr (QNEXT) {  // phase A read the current Q^T for the last time
+            load_q(nxt);
+            fence();
+        }
+        u32x2 vf[VA + 1][2];
+        float m4[4];
+        static_for<VA>([&](auto p_c) { vread_(p_c, SLC{}, vf, vb_e, vb_o); });
+        static_for<18>([&](auto j_c) {
+            constexpr int J = decltype(j_c)::value;
+            constexpr int KK = J / 9, JJ = J % 9;
+            if constexpr (JJ < 8) {
+                constexpr int PP = KK * NDB + JJ;
+                if constexpr (PP + VA < NKK * NDB) vread_(std::integral_constant<int, PP + VA>{}, SLC{}, vf, vb_e, vb_o);
+                constexpr int AFTER = 2 * ((PP + VA < NKK * NDB ? PP + VA : NKK * NDB - 1) - PP);
+                lwait2(std::integral_constant<int, AFTER>{}, vf[PP % (VA + 1)]);
+                const u32x4 vv = {vf[PP % (VA + 1)][0][0], vf[PP % (VA + 1)][0][1], vf[PP % (VA + 1)][1][0],
+                                  vf[PP % (VA + 1)][1][1]};
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb)
+                    o[JJ][qb] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[KK][qb]),
+                                         EPI && KK == 0 ? f32x4{} : o[JJ][qb]);
+            } else {
+#pragma unroll
+                for (int qb = 0; qb < NQB; ++qb)
+                    rs[qb] = M::mma16(ones, __builtin_bit_cast(v8, pbu[KK][qb]), EPI && KK == 0 ? f32x4{} : rs[qb]);
+            }
+            if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
+            if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
+            if constexpr (J >= 1 && J <= 8) cvt(std::integral_constant<int, 8 + J - 1>{});
+            if constexpr (MORE) {
+                if constexpr (J >= 8 && J < 16)
+                    chain_max(sn, std::integral_constant<int, (J - 8) / 2>{}, std::integral_constant<int, (J - 8) % 2>{},
+                              m4[(J - 8) / 2]);
+                if constexpr (J == 16) {
+                    quad_max2(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]), mx[0], mx[1]);
+                    mx[0] *= c;
+                    mx[1] *= c;
+                }
+            }
+            fence();
+        });
+#if FA_CHAIN_TAP
+        // priority for the next step from the real-time clock (issued here, where no LDS read is
+        // in flight: the wait for it cannot be mistaken for an LDS wait)
+        hi = __builtin_amdgcn_readfirstlane(((unsigned)(__builtin_amdgcn_s_memrealtime() >> FA_CHAIN_TAP_SHIFT) ^ tgp) & 1);
+#endif
+        if constexpr (QNEXT) {
+            // the K / V pieces issued before the Q loads have landed (their 2 * DPW pieces are
+            // older than the 8 Q loads); the Q loads stay in flight into the next step, whose
+            // first QK^T MFMA the compiler makes wait for them
+            static_assert(NQB * NKS == 8, "vmcnt count of the Q loads");
+            asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        } else {
+            __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
+        }
+        if constexpr (QPF) asm volatile("" ::"v"(pf));
+    };
+
+    // prologue of the first item (fa_fwd16_kernel.hpp's)
+    Item cur = item(0);
+    load_q(cur);
+    dma_tile(cur.k, kring, 0);
+    dma_tile(cur.v, vring, 0);
+    dma_tile(cur.k, kring + TILEB, 1);
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[qb][ks]));
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPW) : "memory");
+    f32x4 sa[NKB][NQB], sb[NKB][NQB];
+    float mx[NQB];
+    qk_all(std::integral_constant<int, 0>{}, sa);
+    rowmax_all(sa, mx);
+    m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
+    m[1] = mx[1];
+    __syncthreads();
+
+    // Every item runs the same step sequence (no branch between variants: a diamond of
+    // whole steps made the register allocator spill the Q^T fragments): step 0 stores the
+    // previous item's O (for the first item into an empty range: the stores are dropped) and
+    // starts O and the row sums from zero, the pair before the last pulls the next Q toward L2,
+    // the last pair fetches the next item's K(0), K(1), V(0) and Q^T and computes its S(0).
+    // After the last item the "next" is an empty range: zero tiles, a discarded S(0).
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using STEADY = std::integral_constant<int, 1 | 4>;
+    const __amdgpu_buffer_rsrc_t none = make_rsrc32(cur.k, 0);
+    __amdgpu_buffer_rsrc_t prev_o = none;  // O tile of the previous item
+    for (int j = 0;; ++j) {
+        const bool more = j + 1 < nmine;
+        const Item nxt = item(more ? j + 1 : j);
+        step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
+             nxt, prev_o);
+        step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, 3), tile_rsrc(cur.v, 2), nxt, none);
+        int t = 2;
+        for (; t + 4 < ntiles; t += 2) {
+            step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(cur.k, t + 2), tile_rsrc(cur.v, t + 1), nxt, none);
+            step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, none);
+        }
+        // t = ntiles - 4: the next item's Q toward L2
+        step(C0{}, std::integral_constant<int, 1 | 4 | (FA_CHAIN_QPF ? 16 : 0)>{}, sa, sb, mx, tile_rsrc(cur.k, t + 2),
+             tile_rsrc(cur.v, t + 1), nxt, none);
+        step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, none);
+        t += 2;
+        // t = ntiles - 2: K(t+2) = the next item's K(0) into K slot 0, V(t+1) ours; the next
+        // Q^T loaded in phase B.  t = ntiles - 1: K(t+2) = next K(1) into slot 1, V(t+1) = next
+        // V(0) into slot 0; QK^T(next 0) -> sa
+        step(C0{}, std::integral_constant<int, 1 | 4 | 8>{}, sa, sb, mx, more ? tile_rsrc(nxt.k, 0) : none,
+             tile_rsrc(cur.v, t + 1), nxt, none);
+        step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none, more ? tile_rsrc(nxt.v, 0) : none, nxt,
+             none);
+        // this item's O stays in the registers until the next item's step 0 stores it
+        einv[0] = 1.f / rs[0][0];
+        einv[1] = 1.f / rs[1][0];
+        m[0] = mx[0];
+        m[1] = mx[1];
+        prev_o = o_rsrc(cur);
+        if (!more) break;
+        cur = nxt;
+    }
+    static_for<8>([&](auto g_c) { store_group(g_c, prev_o); });
+}
+
+}  // namespace fa

@@ -129,6 +129,8 @@ hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStrea
 // the strided instantiations (fa_fwd_strided.hip); launch_fwd forwards there when a.strided
 hipError_t launch_fwd_strided(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
+// compute units of the current device (fa_capi.cpp; 256 without a device)
+int device_cus();
 // fp64 mode (fa_fwd64.hip): 64 query rows x 16-key tiles; final or row-layout partial
 hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s);

@@ -39,22 +39,24 @@ def _device_inputs(L, d, seed):
     return [torch.randn(B, H, L, d, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3)]
 
 
-def _check_sampled(out, q, k, v):
-    """The gates of test_gpu on the sampled heads (fp64 oracle on the same bf16 inputs)."""
+def _check_sampled(out, q, k, v, label=None):
+    """The gates of test_gpu on the sampled heads (fp64 oracle on the same bf16 inputs); with a
+    label, the elements over the waived bf16 max_rel gate are recorded (test_gpu.MAXREL_WAIVER)."""
     assert bool(torch.isfinite(out).all())
     heads = _sample()
     pick = lambda t: torch.stack([t[b, h] for b, h in heads])[None].cpu()  # [1, 16, L, d]
     qs, ks, vs, os_ = (pick(t) for t in (q, k, v, out))
     ref = attention_fp64(qs.double().numpy(), ks.double().numpy(), vs.double().numpy())
-    return _gate(os_, ref, torch.bfloat16)
+    return _gate(os_, ref, torch.bfloat16, label=label)
 
 
 @pytest.mark.parametrize("d", [32, 128], ids=["C2", "C3"])
 def test_fullsize_v1_and_tiled_d(gpu, d):
     from exploring_flash_attention_amd import ops
     q, k, v = _device_inputs(1024, d, seed=d)
-    _check_sampled(ops.attention_v1(q, k, v), q, k, v)
-    _check_sampled(ops.attention_tiled_d(q, k, v, 32, 32), q, k, v)
+    name = {32: "C2", 128: "C3"}[d]
+    _check_sampled(ops.attention_v1(q, k, v), q, k, v, label=f"fullsize {name} v1 (16 heads)")
+    _check_sampled(ops.attention_tiled_d(q, k, v, 32, 32), q, k, v, label=f"fullsize {name} tiled-d (16 heads)")
 
 
 @pytest.mark.parametrize("kvt,group", [(4, None), (4, 1), (4, 4), ("auto", None)],
@@ -74,7 +76,7 @@ def test_fullsize_c4_splitkv(gpu, kvt, group):
     o2 = ops.attention_v2(q, k, v, kvt, workspace=ws, blocks_per_workgroup=group)
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)  # the combine order is fixed: bitwise repeatable
-    _check_sampled(o1, q, k, v)
+    _check_sampled(o1, q, k, v, label=f"fullsize C4 kvtpb={kvt} group={group} (16 heads)")
 
 
 def _driver_inputs(oracle_lib, L, d):
@@ -162,3 +164,54 @@ def test_sdpa_crosscheck_c3(gpu):
     assert float((ours.float() - sdpa.float()).abs().max()) <= 2 * 6e-3
     # no worse than the library reference beyond a bf16 rounding step
     assert m_ours["max_abs"] <= max(6e-3, 1.5 * m_sdpa["max_abs"]), (m_ours, m_sdpa)
+
+
+def test_fullsize_c5_splitkv_emulated_w8(gpu):
+    """C5 -- B32 H8 L16384 d128, the keys sharded over W = 8 ranks -- at its full per-rank
+    size on ONE GPU, every rank's kernels run in turn:
+
+    * rank p (key shard p) computes its scaled-fp16 partials one destination chunk at a time
+      from row-range views of q, exactly as the overlapped exchange does
+      (dist._exchange_overlapped -> dist._partial_chunk_fn), and the chunks are placed where
+      the exchange delivers them: rank j's receive buffer [W][B*H][L/W][d], slot p;
+    * each shard's chunks are bitwise equal to the all-to-all form's one-launch partial in the
+      send layout (dist._partial_fn, overlap=False), so both exchanges hand the combine the
+      same bytes;
+    * rank j's combine (dist._combine_fn, the reduction of
+      flash_attention_v2/CUDA/flash_attention_v2.h:356-435 over the 8 shards) gives its query
+      rows; sampled heads (first and last included) x 32 sampled rows of EVERY rank's chunk
+      (first and last rows included) against the fp64 oracle.
+    The RCCL transfer itself is covered by test_gpu_multirank.py (one GPU per rank)."""
+    from exploring_flash_attention_amd import dist as fdist
+    from exploring_flash_attention_amd import ops
+    W, L, d = 8, 16384, 128
+    Lc = L // W
+    q, k, v = _device_inputs(L, d, seed=5)
+    fp16s = ops.PARTIAL_FP16_SCALED
+    o_recv = torch.empty((W, W, B * H, Lc, d), dtype=torch.float16, device=gpu)  # [rank j][from p]
+    lse_recv = torch.empty((W, W, B * H, Lc, 2), dtype=torch.float32, device=gpu)
+    for p in range(W):
+        ks = k[:, :, p * Lc:(p + 1) * Lc].contiguous()
+        vs = v[:, :, p * Lc:(p + 1) * Lc].contiguous()
+        for j in range(W):
+            fdist._partial_chunk_fn(q[:, :, j * Lc:(j + 1) * Lc], ks, vs, o_recv[j, p], lse_recv[j, p], fp16s)
+        o_a2a, lse_a2a = fdist._partial_fn(q, ks, vs, Lc, fp16s)  # [W][B*H][Lc][d] send layout
+        torch.cuda.synchronize()
+        assert torch.equal(o_a2a, o_recv[:, p]) and torch.equal(lse_a2a, lse_recv[:, p]), p
+        del ks, vs, o_a2a, lse_a2a
+    rows = sorted({j * Lc + round(i * (Lc - 1) / 31) for j in range(W) for i in range(32)})
+    picked = []
+    for j in range(W):
+        oj = fdist._combine_fn(o_recv[j], lse_recv[j], B, H, q.dtype)  # [B, H, Lc, d]
+        assert oj.shape == (B, H, Lc, d) and oj.dtype == q.dtype
+        picked.append(oj[:, :, [r - j * Lc for r in rows if j * Lc <= r < (j + 1) * Lc]])
+    torch.cuda.synchronize()
+    del o_recv, lse_recv
+    out_rows = torch.cat(picked, dim=2)  # [B, H, len(rows), d]
+    assert bool(torch.isfinite(out_rows).all())
+    heads = _sample()
+    pick = lambda t: torch.stack([t[b, h] for b, h in heads])[None].cpu()
+    qs = pick(q[:, :, rows])
+    ks, vs, os_ = pick(k), pick(v), pick(out_rows)
+    ref = attention_fp64(qs.double().numpy(), ks.double().numpy(), vs.double().numpy())
+    _gate(os_, ref, torch.bfloat16, label="fullsize C5 W=8 emulated (16 heads x 256 rows)")

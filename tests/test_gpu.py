@@ -39,15 +39,43 @@ def _ref(q, k, v):
     return attention_fp64(q.double().numpy(), k.double().numpy(), v.double().numpy())
 
 
-def _gate(out, ref, dtype):
+# bf16 max_rel waiver records (conftest.py prints them in the terminal summary): the
+# reference's third gate (max_rel 0.5 over |ref| > 1e-3, common/reference.py:24-78) is not
+# applied to bf16; every element that would fail it is counted here and must still meet the
+# bf16 build gate's max_abs
+MAXREL_WAIVER = []
+
+
+def _maxrel_violators(out, ref, label):
+    """Elements over the reference's max_rel 0.5 (|ref| > 1e-3): count, out of how many, and
+    their largest |ref| and |err|."""
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(out.astype(np.float64) - ref)
+    big = np.abs(ref) > 1e-3
+    bad = big & (err > 0.5 * np.abs(ref))
+    rec = {"label": label, "count": int(bad.sum()), "of": int(big.sum()),
+           "max_abs_ref": float(np.abs(ref[bad]).max()) if bad.any() else None,
+           "max_err": float(err[bad].max()) if bad.any() else None,
+           "max_rel": float((err[bad] / np.abs(ref[bad])).max()) if bad.any() else None}
+    return rec, bool((err[bad] <= GATE[torch.bfloat16][0]).all())
+
+
+def _gate(out, ref, dtype, label=None):
     out = out.float().cpu().numpy()
     assert np.isfinite(out).all()
-    # hard gate (raises); for bf16 the max_rel term is reported, not gated: outputs that are
-    # cancellations near the |ref| > 1e-3 filter carry bf16-sized absolute error
+    # hard gate (raises); for bf16 the max_rel term is not gated -- outputs that are
+    # cancellations near the |ref| > 1e-3 filter carry bf16-sized absolute error -- but every
+    # element over it is counted (MAXREL_WAIVER) and must meet the bf16 build gate's max_abs
     m = check_accuracy(out, ref, max_rel_tol=0.5 if dtype == torch.float16 else float("inf"))
     max_abs, mean_rel = GATE[dtype]
     assert m["max_abs"] <= max_abs, m
     assert m["mean_rel"] is None or m["mean_rel"] <= mean_rel, m
+    if dtype == torch.bfloat16:
+        rec, within = _maxrel_violators(out, ref, label or "")
+        m["max_rel_violators"] = rec
+        if label is not None:
+            MAXREL_WAIVER.append(rec)
+        assert within, rec
     return m
 
 
@@ -174,7 +202,7 @@ def test_matrix(gpu, variant, dtype, d):
         out = fn(q.to(gpu), k.to(gpu), v.to(gpu))
         torch.cuda.synchronize()
         assert out.shape == q.shape and out.dtype == dtype
-        _gate(out, _ref(q, k, v), dtype)
+        _gate(out, _ref(q, k, v), dtype, label=f"matrix {variant} d={d} B{B}H{H}L{L}")
 
 
 @pytest.mark.parametrize("d", [32, 64, 128, 256])

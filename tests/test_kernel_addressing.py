@@ -285,3 +285,55 @@ def test_dtiled_kernel_in_bounds(B, H, L, d, dq, dv):
     rows = q_tile0[:, None] + np.arange(64)[None, :]
     live = rows < L
     o.check(np.where(live, 2 * (bh[:, None] * L * D + rows * D), 0), np.where(live, ROWD, 0), "O row store")
+
+
+def chain_items(nitems, grid):
+    """fa_fwd16_chain.hpp's static schedule: block b serves XCD group b % 8 and takes items
+    l, l + G/8, ... (l = b / 8) of the contiguous range xcd_remap gives the group."""
+    nl = grid >> 3
+    iq, ir = nitems >> 3, nitems & 7
+    out = []
+    for b in range(grid):
+        x, l = b & 7, b >> 3
+        gstart = x * (iq + 1) if x < ir else ir * (iq + 1) + (x - ir) * iq
+        gcnt = iq + (1 if x < ir else 0)
+        nmine = (gcnt - l + nl - 1) // nl if l < gcnt else 0
+        out.append([gstart + l + nl * j for j in range(nmine)])
+    return out
+
+
+@pytest.mark.parametrize("cus", [256, 304, 80])
+@pytest.mark.parametrize("B,H,L", [(32, 8, 1024), (32, 8, 2048), (32, 8, 4096), (4, 32, 1024), (16, 2, 384),
+                                   (3, 7, 1408)],
+                         ids=["C3", "L2048", "C4-unsplit", "b4h32", "l384", "odd-heads"])
+def test_chain_kernel_items_and_bounds(B, H, L, cus):
+    """The chained persistent kernel (d = 128 final mode, fa_fwd16_chain.hpp): under the
+    launcher's conditions (fa_fwd.hip launch_one: Lk % 128 == 0, Lk >= 384, Lq % 128 == 0, a
+    grid of 2 workgroups per CU rounded down to a multiple of 8, at most one workgroup per
+    query tile) every query tile is run by exactly one workgroup, no workgroup runs none (the
+    kernel returns early only then), and every descriptor it builds -- Q, the K / V tiles
+    0..ntiles-1 of the item and K(0), K(1), V(0) of the next, the Q prefetch dwords, the O
+    tile -- lies inside its tensor."""
+    D, ROWB, BK, TILEB = 128, 256, 64, 64 * 256
+    nqt, BH = L // KBQ, B * H
+    nitems = nqt * BH
+    grid = 2 * cus // 8 * 8
+    if not (L % 128 == 0 and L >= 384 and L % KBQ == 0 and nitems >= grid):
+        pytest.skip("the launcher runs the one-shot kernel for this shape")
+    lists = chain_items(nitems, grid)
+    flat = [w for lst in lists for w in lst]
+    assert sorted(flat) == list(range(nitems)), "items not covered exactly once"
+    assert all(len(lst) > 0 for lst in lists)
+    assert max(map(len, lists)) - min(map(len, lists)) <= 1 + (nitems % grid != 0)
+    q, k, v, o = (_tensor(n, B, H, L, D) for n in "qkvo")
+    ntiles = L // BK
+    w = np.array(flat, dtype=np.int64)
+    qt, bh = w % nqt, w // nqt
+    qoff = 2 * (bh * L + qt * KBQ) * D
+    q.check(qoff, KBQ * ROWB, "chain Q tile")
+    q.check(qoff + (3 * 64 + 63) * 128, 4, "chain Q prefetch dword")
+    o.check(qoff, KBQ * ROWB, "chain O tile")
+    kv0 = 2 * bh * L * D
+    for t in range(ntiles):
+        k.check(kv0 + t * TILEB, TILEB, "chain K tile")
+        v.check(kv0 + t * TILEB, TILEB, "chain V tile")
