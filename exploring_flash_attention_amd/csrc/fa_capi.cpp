@@ -15,7 +15,30 @@
 #include "../../include/fa_mi355x.h"
 #include "fa_internal.hpp"
 
+namespace fa {
+// Compute units of the current device, queried once per device (the split planner runs on
+// every fa_fwd_v2 call).  No device (CPU-only tests): the MI355X's 256.
+int device_cus() {
+    static std::atomic<int> cached[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return 256;
+    }
+    int n = cached[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 256;
+    }
+    cached[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
+}  // namespace fa
+
 namespace {
+
+using fa::device_cus;
 
 thread_local std::string g_err;
 
@@ -210,24 +233,6 @@ V2Layout v2_layout(int64_t BH, int64_t L, int64_t d, int ns, fa::Elem pe) {
     return w;
 }
 
-// Compute units of the current device, queried once per device (the split planner runs on
-// every fa_fwd_v2 call).  No device (CPU-only tests): the MI355X's 256.
-int device_cus() {
-    static std::atomic<int> cached[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-        (void)hipGetLastError();
-        return 256;
-    }
-    int n = cached[dev].load(std::memory_order_relaxed);
-    if (n > 0) return n;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
-        (void)hipGetLastError();
-        n = 256;
-    }
-    cached[dev].store(n, std::memory_order_relaxed);
-    return n;
-}
 
 // How many partial workgroups per query tile the split-KV schedule wants: none beyond the
 // first when the query tiles alone give every CU a workgroup, otherwise enough for one per CU.

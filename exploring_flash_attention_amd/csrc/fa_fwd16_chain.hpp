@@ -40,6 +40,21 @@
 #ifndef FA_CHAIN_TAP_SHIFT
 #define FA_CHAIN_TAP_SHIFT 9  // priority period 2^shift x 10 ns (9: 5.12 us)
 #endif
+// Lazy row max: no row max of S(t+1) per step.  The exponentials of tile t use the running
+// reference m (kept FA_LAZY_MARGIN log2 units above the largest score seen when it was last
+// set, so P <= 2^-margin); whether any P of a 32-key step reached 2 is read off the packed
+// 16-bit P itself -- bit 14 (the exponent's top bit in bf16 and fp16) of the OR of the step's
+// packed dwords -- before the P.V MFMAs consume it.  Only then (rare: a score more than
+// margin + 1 above the reference) does a slow path compute the tile's exact row max from the
+// scores (kept intact: the exponentials go to temporaries), raise m, rescale O and the row
+// sums and recompute the tile's P.  Saves the per-step max tree (18 v_maximum3, the permlane
+// reduction, 2 multiplies) for ~6 VALU of test.
+#ifndef FA_LAZYMAX
+#define FA_LAZYMAX 0
+#endif
+#ifndef FA_LAZY_MARGIN
+#define FA_LAZY_MARGIN 3.f
+#endif
 
 namespace fa {
 
@@ -257,7 +272,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // barrier leaves those loads in flight), 16 QPF (the next item's Q is pulled toward L2),
     // 32 EPI (step 0 of an item whose predecessor's O is still in the registers: phase A stores
     // it, one 16-byte row store per even slot, and phase B's first P.V / row-sum MFMAs start
-    // from zero instead of accumulating).
+    // from zero instead of accumulating), 64 ROWMAX (lazy mode: the row max of S(t+1) is computed
+    // anyway -- the next item's S(0), whose reference m starts there).
     auto step = [&](auto par_c, auto flags_c, f32x4 (&sc)[NKB][NQB], f32x4 (&sn)[NKB][NQB], float (&mx)[NQB],
                     __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt,
                     __amdgpu_buffer_rsrc_t ors) {
@@ -268,9 +284,11 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         constexpr bool QNEXT = F & 8;
         constexpr bool QPF = F & 16;
         constexpr bool EPI = F & 32;
+        constexpr bool LAZY = FA_LAZYMAX;
+        constexpr bool RMAX = MORE && (!LAZY || (F & 64));  // row max of S(t+1) in phase B
         using SLN = std::integral_constant<int, 1 - P>;
         using SLC = std::integral_constant<int, P>;
-        if (!EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
+        if (!LAZY && !EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
 #pragma unroll
             for (int qb = 0; qb < NQB; ++qb) {
                 const float m_new = fmaxf(m[qb], mx[qb]);
@@ -294,15 +312,61 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         if constexpr (QPF)  // one dword per 128-byte line of the next tile's Q (256 lines, 4 waves)
             pf = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(uni(nxt.q), nxt.q_rows * ROWB), (wid * 64 + lane) * 128, 0, 0);
 
+        // score e of tile t: key step e / 16, query block (e / 8) & 1, key block 2*(e/16) + (e/4)&1,
+        // reg e&3; in place, or (lazy) into pv so that the scores stay for the slow path
+        f32x4 pv[NKB][NQB];
         auto ex = [&](auto e_c) {
             constexpr int E = decltype(e_c)::value, KK = E / 16, QB = (E / 8) & 1, KB = 2 * KK + ((E / 4) & 1), I = E & 3;
-            sc[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, QB ? nm1 : nm0));
+            if constexpr (LAZY)
+                pv[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, -m[QB]));
+            else
+                sc[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, QB ? nm1 : nm0));
         };
         u32x4 pbu[NKK][NQB];
-        auto cvt = [&](auto k_c) {
+        auto cvt = [&](auto k_c) {  // pack k = exponentials 2k, 2k+1
             constexpr int K = decltype(k_c)::value, KK = K / 8, QB = (K / 4) & 1, J = K % 4;
             constexpr int KB = 2 * KK + (J >> 1), I = 2 * (J & 1);
-            pbu[KK][QB][J] = pack2<T>(sc[KB][QB][I], sc[KB][QB][I + 1]);
+            if constexpr (LAZY)
+                pbu[KK][QB][J] = pack2<T>(pv[KB][QB][I], pv[KB][QB][I + 1]);
+            else
+                pbu[KK][QB][J] = pack2<T>(sc[KB][QB][I], sc[KB][QB][I + 1]);
+        };
+        // lazy: any P of key step kk >= 2 (or inf / NaN): bit 14 of a 16-bit half of the OR
+        auto big = [&](auto kk_c) {
+            constexpr int KK = decltype(kk_c)::value;
+            const u32x4& a0 = pbu[KK][0];
+            const u32x4& a1 = pbu[KK][1];
+            const unsigned x = (a0[0] | a0[1] | a0[2]) | (a0[3] | a1[0] | a1[1]) | (a1[2] | a1[3]);
+            return __builtin_amdgcn_ballot_w64((x & 0x40004000u) != 0) != 0;
+        };
+        // lazy slow path: exact row max of tile t, m raised to it + margin, O (unless SCALE_O is
+        // off: step 0 of an item still storing the previous O) and the row sums rescaled, all of
+        // the tile's P recomputed
+        auto fixup = [&](auto scale_o_c) {
+            constexpr bool SCALE_O = decltype(scale_o_c)::value;
+            float m4[4], mt[NQB];
+            static_for<8>([&](auto i_c) {
+                constexpr int I = decltype(i_c)::value;
+                chain_max(sc, std::integral_constant<int, I / 2>{}, std::integral_constant<int, I % 2>{}, m4[I / 2]);
+            });
+            quad_max2(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]), mt[0], mt[1]);
+#pragma unroll
+            for (int qb = 0; qb < NQB; ++qb) {
+                const float m_new = fmaxf(m[qb], mt[qb] * c + FA_LAZY_MARGIN);
+                const float alpha = __builtin_amdgcn_exp2f(m[qb] - m_new);
+                m[qb] = m_new;
+                if constexpr (SCALE_O) {
+                    rs[qb] *= alpha;
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
+                }
+            }
+            static_for<16>([&](auto k_c) {
+                constexpr int K = decltype(k_c)::value;
+                ex(std::integral_constant<int, 2 * K>{});
+                ex(std::integral_constant<int, 2 * K + 1>{});
+                cvt(k_c);
+            });
         };
         auto dma = [&](auto i_c) {
             constexpr int I = decltype(i_c)::value;
@@ -336,8 +400,13 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                     sn[S % NKB][qb] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[qb][S / NKB], sn[S % NKB][qb]);
             }
             constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;
-            static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
-            if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});
+            static_for<E1 - E0>([&](auto j_c) {
+                constexpr int E = E0 + decltype(j_c)::value;
+                ex(std::integral_constant<int, E>{});
+                if constexpr (LAZY && (E & 1)) cvt(std::integral_constant<int, E / 2>{});  // the pair is done
+            });
+            if constexpr (!LAZY && S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});
+
             if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
             if constexpr (EPI && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ors);
             if constexpr (MORE) fence();
@@ -350,6 +419,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         if constexpr (QNEXT) {  // phase A read the current Q^T for the last time
             load_q(nxt);
             fence();
+        }
+        if constexpr (LAZY) {  // key step 0's P (exponentials 0..15, phase A) before its P.V
+            static_assert(EXPA >= 16, "key step 0 exponentials in phase A");
+            if (big(std::integral_constant<int, 0>{})) fixup(std::integral_constant<bool, !EPI>{});
         }
         u32x2 vf[VA + 1][2];
         float m4[4];
@@ -375,8 +448,16 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             }
             if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
             if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
-            if constexpr (J >= 1 && J <= 8) cvt(std::integral_constant<int, 8 + J - 1>{});
-            if constexpr (MORE) {
+            if constexpr (LAZY && EXPA + 2 * J + 1 < 32) {
+                static_assert(EXPA % 2 == 0, "pairs");
+                cvt(std::integral_constant<int, (EXPA + 2 * J) / 2>{});
+            }
+            if constexpr (!LAZY && J >= 1 && J <= 8) cvt(std::integral_constant<int, 8 + J - 1>{});
+            if constexpr (LAZY && J == (32 - EXPA) / 2) {  // key step 1's P, before its P.V (slot 9)
+                // (key step 0's P.V of slots 0.. J-1 used the old m: the rescale of O covers it)
+                if (big(std::integral_constant<int, 1>{})) fixup(std::integral_constant<bool, true>{});
+            }
+            if constexpr (RMAX) {
                 if constexpr (J >= 8 && J < 16)
                     chain_max(sn, std::integral_constant<int, (J - 8) / 2>{}, std::integral_constant<int, (J - 8) % 2>{},
                               m4[(J - 8) / 2]);
@@ -420,8 +501,9 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     float mx[NQB];
     qk_all(std::integral_constant<int, 0>{}, sa);
     rowmax_all(sa, mx);
-    m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
-    m[1] = mx[1];
+    constexpr float kM0 = FA_LAZYMAX ? FA_LAZY_MARGIN : 0.f;
+    m[0] = mx[0] + kM0;  // the reference max starts at tile 0's row max (no step-0 rescale)
+    m[1] = mx[1] + kM0;
     __syncthreads();
 
     // Every item runs the same step sequence (no branch between variants: a diamond of
@@ -456,13 +538,13 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         // V(0) into slot 0; QK^T(next 0) -> sa
         step(C0{}, std::integral_constant<int, 1 | 4 | 8>{}, sa, sb, mx, more ? tile_rsrc(nxt.k, 0) : none,
              tile_rsrc(cur.v, t + 1), nxt, none);
-        step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none, more ? tile_rsrc(nxt.v, 0) : none, nxt,
-             none);
+        step(C1{}, std::integral_constant<int, 1 | 4 | 64>{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none,
+             more ? tile_rsrc(nxt.v, 0) : none, nxt, none);
         // this item's O stays in the registers until the next item's step 0 stores it
         einv[0] = 1.f / rs[0][0];
         einv[1] = 1.f / rs[1][0];
-        m[0] = mx[0];
-        m[1] = mx[1];
+        m[0] = mx[0] + kM0;
+        m[1] = mx[1] + kM0;
         prev_o = o_rsrc(cur);
         if (!more) break;
         cur = nxt;

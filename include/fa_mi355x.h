@@ -146,8 +146,11 @@ int fa_fwd_v1_tiled_d_scaled(const void* q, const void* k, const void* v, void* 
 
 /* kv_tiles_per_block value that lets the library choose the split from the device's
  * occupancy: no split when the query tiles alone number at least the device's compute units,
- * otherwise about one workgroup per CU (the reference's README presets,
- * flash_attention_v2/README.md:29-32, made automatic). */
+ * otherwise ceil(CUs / query tiles) splits (about one workgroup per CU) -- and, for d = 128
+ * with 16-bit inputs, ceil(2 * CUs / query tiles) splits (two workgroups per CU) whenever
+ * every split then still keeps at least 4096 keys (e.g. B1 H1 L16384: 128 query tiles on 256
+ * CUs -> 4 splits, not 2).  The reference's README presets (flash_attention_v2/README.md:29-32)
+ * made automatic. */
 #define FA_KV_TILES_AUTO (-1)
 
 /* blocks_per_workgroup value that lets the library group the key blocks of a query tile onto
@@ -174,7 +177,9 @@ int fa_fwd_v2_workspace_size_ex(int64_t B, int64_t H, int64_t L, int64_t d,
  * workgroups per query tile (combined through the workspace).  With blocks_per_workgroup =
  * FA_BLOCKS_PER_WG_AUTO the library cuts the blocks of a query tile into equal groups: none beyond
  * one when the query tiles alone number at least the device's compute units, otherwise
- * ceil(CUs / query tiles) groups (about one workgroup per CU; d = 384 / 512: always one group);
+ * ceil(CUs / query tiles) groups (about one workgroup per CU) -- for d = 128 with 16-bit inputs
+ * ceil(2 * CUs / query tiles) groups (two per CU) when each group then keeps >= 4096 keys
+ * (B1 H1 L16384 on 256 CUs: 4 partials per tile); d = 384 / 512: always one group;
  * a positive value fixes the group size (1: one workgroup and one HBM partial per key block, the
  * reference's layout; clamped to the number of blocks).  The plan depends only on the
  * arguments and the device's compute-unit count.  Any output pointer may be NULL. */
