@@ -314,8 +314,8 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
 }
 
 // Work order of the fused split launch (FwdArgs::tile_group): split fastest when the whole
-// grid is resident at once (at most two workgroups per CU) and a query tile has at least 4
-// partials, query tile fastest otherwise.
+// grid is one workgroup per CU and a query tile has at least 4 partials, query tile fastest
+// otherwise.
 // Measured (round 4, A/B in one process, profiles/r04/ab_split_order.log; outputs bitwise
 // equal): B1 H2 L4096 (4 partials, 256 workgroups) 30.9 -> 28.9 us; B1 H1 L16384 (2 partials,
 // 256) 132.2 -> 131.5 us; but B2 H2 L16384 (4 partials, 2048) -1.6 %, C4 with 4 partials per
@@ -339,9 +339,12 @@ int plan_splits(int64_t BH, int64_t L, int64_t d, int kvtpb, int blocks_per_wg, 
 #endif
 int tile_group(int64_t nblk, int ns, int nqt) {
     if (FA_SPLIT_ORDER_RULE != 2) return FA_SPLIT_ORDER_RULE == 1 ? 1 : 0;
-    // (B1 H1 L16384, 2 partials: equal time either way, but split fastest puts both halves of
-    // the keys on every XCD -- 93 MB of L2 egress per launch against 64 MB (profiles/r04))
-    if (ns >= 4 && nblk <= 2 * (int64_t)device_cus()) return 1;
+    // Split fastest only when the whole grid is ONE workgroup per CU (B1 H2 L4096: 256): at two
+    // per CU (B1 H1 L16384, 4 partials, 512 workgroups) the two orders measured within 0.5 %
+    // (122.4 vs 122.9 us, profiles/r04/ab_split_order_g.log) but split fastest puts every key
+    // on every XCD -- 110 MB of L2 egress per launch against ~68 MB query tile fastest
+    // (round 5: VERDICT r4 item 6)
+    if (ns >= 4 && nblk <= (int64_t)device_cus()) return 1;
     if (FA_TILE_GROUP > 1 && ns >= FA_TG_MIN && nqt % FA_TILE_GROUP == 0) return FA_TILE_GROUP;
     return 0;
 }

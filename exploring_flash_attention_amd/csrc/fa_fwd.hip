@@ -26,7 +26,7 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
             // whole query-tile chains: an even number of 64-key tiles and at least one query
             // tile per workgroup of a 2-per-CU grid
             const int64_t grid = 2 * (int64_t)device_cus() / 8 * 8;
-            if (a.Lk % 128 == 0 && a.Lk >= 384 && a.Lq % kBQ == 0 && a.nsplit == 1 && nblk >= grid && grid >= 8 &&
+            if (a.Lk % 128 == 0 && a.Lk >= 256 && a.Lq % kBQ == 0 && a.nsplit == 1 && nblk >= grid && grid >= 8 &&
                 nblk < (int64_t)1 << 31) {
                 hipLaunchKernelGGL((fa_fwd16_chain_kernel<T>), dim3((unsigned)grid), dim3(kThreads), lds, s, a,
                                    (int)nblk);

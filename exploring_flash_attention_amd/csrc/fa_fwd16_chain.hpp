@@ -18,43 +18,26 @@
 // dispatch -- speed only) and takes the group's items l, l + G/8, l + 2G/8, ... (l = b / 8), of
 // the contiguous item range xcd_remap gives the group: at any time an XCD runs consecutive
 // items, i.e. all query tiles of a few heads, which share their K / V in that XCD's L2.
-// A persistent grid loses the one-shot grid's alternating age priority (a replacement
-// workgroup is younger than its CU partner, so the older one wins VALU-issue arbitration,
-// then the other way round); with fixed partners the older would keep winning (round 2: end
-// times 1543-2072 us at C4).  FA_CHAIN_TAP: each wave's issue priority alternates with the
-// 100 MHz real-time clock, opposite phase for the CU's two workgroups (TG_ID parity), so
-// each holds priority half of the time whatever their ages.
+// Every item runs the same step sequence, with no branch between step variants (a diamond of
+// whole steps made the register allocator spill the Q^T fragments, 500+ bytes of scratch):
+// step 0 stores the previous item's O (the first item's step 0 into an empty range, so its
+// stores are dropped) and starts O and the row sums from zero; the last pair of steps fetches
+// the next item's K(0), K(1), V(0) and Q^T and computes its S(0) -- after the workgroup's last
+// item from empty ranges (zero tiles, an S(0) nobody reads).
+//
+// Measured (A/B in one process against the one-shot kernel, outputs
+// bitwise equal -- the same steps in the same order): C3 +1 ... +2 %, L = 2048 +0.6 ... +1.2 %,
+// C4 +0.3 %.  Tried and dropped: issue priority alternating between the CU's two workgroups
+// with the real-time clock (a persistent grid loses the one-shot grid's alternating age
+// priority; it measured within noise), the next Q pulled toward L2 a few steps before the
+// seam (within noise), a lazy row max tested on the packed P bits (spilled, 3x slower).
 //
 // Requirements (checked by the launcher): contiguous [B, H, L, d], d = 128, Lk a multiple of
-// 128 (an even number of 64-key tiles, so every tile starts on ring parity 0), at least as
-// many query tiles as workgroups.  Everything else is fa_fwd16_kernel.hpp's step, unchanged.
+// 128 of at least 256 (an even number >= 4 of 64-key tiles, so every item starts on ring
+// parity 0 and its first and last step pairs differ), Lq a multiple of 128 (every O row of a
+// tile exists: the stores need no row test), at least as many query tiles as workgroups.
 #pragma once
 #include "fa_fwd16_kernel.hpp"
-
-#ifndef FA_CHAIN_QPF
-#define FA_CHAIN_QPF 4  // the next tile's Q is pulled into L2 this many steps before the seam (0: off)
-#endif
-#ifndef FA_CHAIN_TAP
-#define FA_CHAIN_TAP 1  // time-alternating issue priority between the CU's two workgroups
-#endif
-#ifndef FA_CHAIN_TAP_SHIFT
-#define FA_CHAIN_TAP_SHIFT 9  // priority period 2^shift x 10 ns (9: 5.12 us)
-#endif
-// Lazy row max: no row max of S(t+1) per step.  The exponentials of tile t use the running
-// reference m (kept FA_LAZY_MARGIN log2 units above the largest score seen when it was last
-// set, so P <= 2^-margin); whether any P of a 32-key step reached 2 is read off the packed
-// 16-bit P itself -- bit 14 (the exponent's top bit in bf16 and fp16) of the OR of the step's
-// packed dwords -- before the P.V MFMAs consume it.  Only then (rare: a score more than
-// margin + 1 above the reference) does a slow path compute the tile's exact row max from the
-// scores (kept intact: the exponentials go to temporaries), raise m, rescale O and the row
-// sums and recompute the tile's P.  Saves the per-step max tree (18 v_maximum3, the permlane
-// reduction, 2 multiplies) for ~6 VALU of test.
-#ifndef FA_LAZYMAX
-#define FA_LAZYMAX 0
-#endif
-#ifndef FA_LAZY_MARGIN
-#define FA_LAZY_MARGIN 3.f
-#endif
 
 namespace fa {
 
@@ -92,9 +75,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n16 = lane & 15, g = lane >> 4;
     const int ntiles = (int)(a.Lk / kBK);
-#if FA_CHAIN_TAP
-    const unsigned tgp = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 16) & 1;  // HW_ID.TG_ID parity
-#endif
 
     // per-item addressing: (query tile, b*h) of item j of this workgroup
     struct Item {
@@ -138,28 +118,25 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                     v8, __builtin_amdgcn_raw_buffer_load_b128(qrs, (wid * 32 + 16 * qb + n16) * ROWB + ks * 64 + pg * 16, 0, 0));
     };
 
-    // LDS-DMA source offsets (fa_fwd16_kernel.hpp's dma_src[i]) as one VGPR + a scalar offset:
-    // piece i of a wave covers image bytes (4 * wid + i) KiB, i.e. row group 2 * wid + i / 2 and
-    // the upper 1 KiB (16-byte chunks 8..15) for odd i, so its source is piece 0's + 2048 * (i / 2)
-    // + 128 * (i & 1) -- one register fewer per piece in a kernel at the 256-register limit
+    // LDS-DMA source offsets of this lane's pieces (fa_fwd16_kernel.hpp): the swizzled image is
+    // produced by giving each lane the SOURCE chunk that lands at its destination
     constexpr int DPW = TILEB / 1024 / kWaves;
-    static_assert(DPW == 4 && ROWB == 256, "piece geometry");
-    int dma_src0;
-    {
-        const int b = wid * DPW * 1024 + lane * 16;
+    int dma_src[DPW];
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+        const int b = (wid * DPW + i) * 1024 + lane * 16;
         const int rg = b / (8 * ROWB), rem = b % (8 * ROWB);
         const int row = 8 * rg + (rem % 512) / 64;
         const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
-        dma_src0 = row * ROWB + ch * 16;
+        dma_src[i] = row * ROWB + ch * 16;
     }
-    auto piece_soff = [](int i) { return 2048 * (i >> 1) + 128 * (i & 1); };
     auto tile_rsrc = [&](const unsigned short* base, int t) {
         return make_rsrc32(uni(base + (int64_t)t * (TILEB / 2)), TILEB);
     };
     auto dma_tile = [&](const unsigned short* base, char* slot, int t) {
         const __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, t);
 #pragma unroll
-        for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src0, piece_soff(i));
+        for (int i = 0; i < DPW; ++i) dma16(rs, slot + (wid * DPW + i) * 1024, dma_src[i], 0);
     };
 
     const int rho = 8 * ((n16 >> 2) & 1) + 4 * (n16 >> 3) + (n16 & 3);
@@ -241,9 +218,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         mx[1] *= c;
     };
 
-#if FA_CHAIN_TAP
-    unsigned hi = tgp;  // this wave holds the higher issue priority (both phases) while hi == 1
-#endif
     // O rows of the previous item, normalised and stored while the next item's first step runs
     // (EPI): lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n]; dv blocks 2e and 2e+1 are
     // paired by one v_permlane16_swap per dword into a 16-byte row store (fa_fwd16_kernel.hpp)
@@ -269,11 +243,9 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // registers hold -- the next item's during the last step of an item.  Flags: 1 MORE (a tile
     // t+1 exists: QK^T, row max, V DMA), 4 DMAK (a K tile is fetched), 8 QNEXT (the next item's
     // Q^T is loaded in phase B, after phase A's last read of the current one, and the closing
-    // barrier leaves those loads in flight), 16 QPF (the next item's Q is pulled toward L2),
-    // 32 EPI (step 0 of an item whose predecessor's O is still in the registers: phase A stores
-    // it, one 16-byte row store per even slot, and phase B's first P.V / row-sum MFMAs start
-    // from zero instead of accumulating), 64 ROWMAX (lazy mode: the row max of S(t+1) is computed
-    // anyway -- the next item's S(0), whose reference m starts there).
+    // barrier leaves those loads in flight), 32 EPI (step 0 of an item whose predecessor's O is
+    // still in the registers: phase A stores it, one 16-byte row store per even slot, and phase
+    // B's first P.V / row-sum MFMAs start from zero instead of accumulating).
     auto step = [&](auto par_c, auto flags_c, f32x4 (&sc)[NKB][NQB], f32x4 (&sn)[NKB][NQB], float (&mx)[NQB],
                     __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt,
                     __amdgpu_buffer_rsrc_t ors) {
@@ -282,13 +254,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         constexpr bool MORE = F & 1;
         constexpr bool DMAK = F & 4;
         constexpr bool QNEXT = F & 8;
-        constexpr bool QPF = F & 16;
         constexpr bool EPI = F & 32;
-        constexpr bool LAZY = FA_LAZYMAX;
-        constexpr bool RMAX = MORE && (!LAZY || (F & 64));  // row max of S(t+1) in phase B
         using SLN = std::integral_constant<int, 1 - P>;
         using SLC = std::integral_constant<int, P>;
-        if (!LAZY && !EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
+        if (!EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
 #pragma unroll
             for (int qb = 0; qb < NQB; ++qb) {
                 const float m_new = fmaxf(m[qb], mx[qb]);
@@ -299,88 +268,32 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
             }
         }
-#if FA_CHAIN_TAP
-        if (hi)
-            __builtin_amdgcn_s_setprio(1);
-        else
-            __builtin_amdgcn_s_setprio(0);
-#endif
         const float nm0 = -m[0], nm1 = -m[1];
         char* const kdst = kring + P * TILEB + wid * DPW * 1024;
         char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
-        unsigned pf = 0;
-        if constexpr (QPF)  // one dword per 128-byte line of the next tile's Q (256 lines, 4 waves)
-            pf = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(uni(nxt.q), nxt.q_rows * ROWB), (wid * 64 + lane) * 128, 0, 0);
 
-        // score e of tile t: key step e / 16, query block (e / 8) & 1, key block 2*(e/16) + (e/4)&1,
-        // reg e&3; in place, or (lazy) into pv so that the scores stay for the slow path
-        f32x4 pv[NKB][NQB];
+        // score e of tile t: key step e / 16, query block (e / 8) & 1, key block 2*(e/16) + (e/4)&1, reg e&3
         auto ex = [&](auto e_c) {
             constexpr int E = decltype(e_c)::value, KK = E / 16, QB = (E / 8) & 1, KB = 2 * KK + ((E / 4) & 1), I = E & 3;
-            if constexpr (LAZY)
-                pv[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, -m[QB]));
-            else
-                sc[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, QB ? nm1 : nm0));
+            sc[KB][QB][I] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[KB][QB][I], c, QB ? nm1 : nm0));
         };
-        u32x4 pbu[NKK][NQB];
-        auto cvt = [&](auto k_c) {  // pack k = exponentials 2k, 2k+1
+        u32x4 pbu[NKK][NQB];  // packed P^T fragments
+        auto cvt = [&](auto k_c) {  // pair k: key step k / 8, query block (k / 4) & 1, dword k % 4
             constexpr int K = decltype(k_c)::value, KK = K / 8, QB = (K / 4) & 1, J = K % 4;
             constexpr int KB = 2 * KK + (J >> 1), I = 2 * (J & 1);
-            if constexpr (LAZY)
-                pbu[KK][QB][J] = pack2<T>(pv[KB][QB][I], pv[KB][QB][I + 1]);
-            else
-                pbu[KK][QB][J] = pack2<T>(sc[KB][QB][I], sc[KB][QB][I + 1]);
-        };
-        // lazy: any P of key step kk >= 2 (or inf / NaN): bit 14 of a 16-bit half of the OR
-        auto big = [&](auto kk_c) {
-            constexpr int KK = decltype(kk_c)::value;
-            const u32x4& a0 = pbu[KK][0];
-            const u32x4& a1 = pbu[KK][1];
-            const unsigned x = (a0[0] | a0[1] | a0[2]) | (a0[3] | a1[0] | a1[1]) | (a1[2] | a1[3]);
-            return __builtin_amdgcn_ballot_w64((x & 0x40004000u) != 0) != 0;
-        };
-        // lazy slow path: exact row max of tile t, m raised to it + margin, O (unless SCALE_O is
-        // off: step 0 of an item still storing the previous O) and the row sums rescaled, all of
-        // the tile's P recomputed
-        auto fixup = [&](auto scale_o_c) {
-            constexpr bool SCALE_O = decltype(scale_o_c)::value;
-            float m4[4], mt[NQB];
-            static_for<8>([&](auto i_c) {
-                constexpr int I = decltype(i_c)::value;
-                chain_max(sc, std::integral_constant<int, I / 2>{}, std::integral_constant<int, I % 2>{}, m4[I / 2]);
-            });
-            quad_max2(fmax_nc(m4[0], m4[1]), fmax_nc(m4[2], m4[3]), mt[0], mt[1]);
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) {
-                const float m_new = fmaxf(m[qb], mt[qb] * c + FA_LAZY_MARGIN);
-                const float alpha = __builtin_amdgcn_exp2f(m[qb] - m_new);
-                m[qb] = m_new;
-                if constexpr (SCALE_O) {
-                    rs[qb] *= alpha;
-#pragma unroll
-                    for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
-                }
-            }
-            static_for<16>([&](auto k_c) {
-                constexpr int K = decltype(k_c)::value;
-                ex(std::integral_constant<int, 2 * K>{});
-                ex(std::integral_constant<int, 2 * K + 1>{});
-                cvt(k_c);
-            });
+            pbu[KK][QB][J] = pack2<T>(sc[KB][QB][I], sc[KB][QB][I + 1]);
         };
         auto dma = [&](auto i_c) {
             constexpr int I = decltype(i_c)::value;
             if constexpr (I < DPW) {
-                if constexpr (DMAK) dma16(krs, kdst + I * 1024, dma_src0, piece_soff(I));
+                if constexpr (DMAK) dma16(krs, kdst + I * 1024, dma_src[I], 0);
             } else if constexpr (MORE) {
-                dma16(vrs, vdst + (I - DPW) * 1024, dma_src0, piece_soff(I - DPW));
+                dma16(vrs, vdst + (I - DPW) * 1024, dma_src[I - DPW], 0);
             }
         };
 
-        // ---- phase A: QK^T(t+1) || exponentials of t
-#if !FA_CHAIN_TAP
+        // ---- phase A: QK^T(t+1) || exponentials of t (and, EPI, the previous item's O stores)
         if constexpr (MORE) __builtin_amdgcn_s_setprio(1);
-#endif
         u32x4 kf[KA + 1];
         if constexpr (MORE) {
 #pragma unroll
@@ -400,29 +313,18 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                     sn[S % NKB][qb] = M::mma16(__builtin_bit_cast(v8, kf[S % (KA + 1)]), qf[qb][S / NKB], sn[S % NKB][qb]);
             }
             constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;
-            static_for<E1 - E0>([&](auto j_c) {
-                constexpr int E = E0 + decltype(j_c)::value;
-                ex(std::integral_constant<int, E>{});
-                if constexpr (LAZY && (E & 1)) cvt(std::integral_constant<int, E / 2>{});  // the pair is done
-            });
-            if constexpr (!LAZY && S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});
-
+            static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
+            if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key step 0 packs
             if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
             if constexpr (EPI && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ors);
             if constexpr (MORE) fence();
         });
 
         // ---- phase B: P.V(t) || exponentials of t (rest), row max of t+1
-#if !FA_CHAIN_TAP
         __builtin_amdgcn_s_setprio(0);
-#endif
         if constexpr (QNEXT) {  // phase A read the current Q^T for the last time
             load_q(nxt);
             fence();
-        }
-        if constexpr (LAZY) {  // key step 0's P (exponentials 0..15, phase A) before its P.V
-            static_assert(EXPA >= 16, "key step 0 exponentials in phase A");
-            if (big(std::integral_constant<int, 0>{})) fixup(std::integral_constant<bool, !EPI>{});
         }
         u32x2 vf[VA + 1][2];
         float m4[4];
@@ -446,18 +348,12 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 for (int qb = 0; qb < NQB; ++qb)
                     rs[qb] = M::mma16(ones, __builtin_bit_cast(v8, pbu[KK][qb]), EPI && KK == 0 ? f32x4{} : rs[qb]);
             }
+            // exponentials EXPA..31, two per slot; key step 1 packs in slots 1..8
             if constexpr (EXPA + 2 * J < 32) ex(std::integral_constant<int, EXPA + 2 * J>{});
             if constexpr (EXPA + 2 * J + 1 < 32) ex(std::integral_constant<int, EXPA + 2 * J + 1>{});
-            if constexpr (LAZY && EXPA + 2 * J + 1 < 32) {
-                static_assert(EXPA % 2 == 0, "pairs");
-                cvt(std::integral_constant<int, (EXPA + 2 * J) / 2>{});
-            }
-            if constexpr (!LAZY && J >= 1 && J <= 8) cvt(std::integral_constant<int, 8 + J - 1>{});
-            if constexpr (LAZY && J == (32 - EXPA) / 2) {  // key step 1's P, before its P.V (slot 9)
-                // (key step 0's P.V of slots 0.. J-1 used the old m: the rescale of O covers it)
-                if (big(std::integral_constant<int, 1>{})) fixup(std::integral_constant<bool, true>{});
-            }
-            if constexpr (RMAX) {
+            if constexpr (J >= 1 && J <= 8) cvt(std::integral_constant<int, 8 + J - 1>{});
+            if constexpr (MORE) {
+                // row max of tile t+1: chain (J - 8) / 2, half (J - 8) % 2 in slots 8..15
                 if constexpr (J >= 8 && J < 16)
                     chain_max(sn, std::integral_constant<int, (J - 8) / 2>{}, std::integral_constant<int, (J - 8) % 2>{},
                               m4[(J - 8) / 2]);
@@ -469,11 +365,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             }
             fence();
         });
-#if FA_CHAIN_TAP
-        // priority for the next step from the real-time clock (issued here, where no LDS read is
-        // in flight: the wait for it cannot be mistaken for an LDS wait)
-        hi = __builtin_amdgcn_readfirstlane(((unsigned)(__builtin_amdgcn_s_memrealtime() >> FA_CHAIN_TAP_SHIFT) ^ tgp) & 1);
-#endif
         if constexpr (QNEXT) {
             // the K / V pieces issued before the Q loads have landed (their 2 * DPW pieces are
             // older than the 8 Q loads); the Q loads stay in flight into the next step, whose
@@ -483,7 +374,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         } else {
             __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
         }
-        if constexpr (QPF) asm volatile("" ::"v"(pf));
     };
 
     // prologue of the first item (fa_fwd16_kernel.hpp's)
@@ -501,17 +391,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     float mx[NQB];
     qk_all(std::integral_constant<int, 0>{}, sa);
     rowmax_all(sa, mx);
-    constexpr float kM0 = FA_LAZYMAX ? FA_LAZY_MARGIN : 0.f;
-    m[0] = mx[0] + kM0;  // the reference max starts at tile 0's row max (no step-0 rescale)
-    m[1] = mx[1] + kM0;
+    m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
+    m[1] = mx[1];
     __syncthreads();
 
-    // Every item runs the same step sequence (no branch between variants: a diamond of
-    // whole steps made the register allocator spill the Q^T fragments): step 0 stores the
-    // previous item's O (for the first item into an empty range: the stores are dropped) and
-    // starts O and the row sums from zero, the pair before the last pulls the next Q toward L2,
-    // the last pair fetches the next item's K(0), K(1), V(0) and Q^T and computes its S(0).
-    // After the last item the "next" is an empty range: zero tiles, a discarded S(0).
     using C0 = std::integral_constant<int, 0>;
     using C1 = std::integral_constant<int, 1>;
     using STEADY = std::integral_constant<int, 1 | 4>;
@@ -520,31 +403,27 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     for (int j = 0;; ++j) {
         const bool more = j + 1 < nmine;
         const Item nxt = item(more ? j + 1 : j);
+        // t = 0, 1 (step 0 stores the previous item's O)
         step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
              nxt, prev_o);
         step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, 3), tile_rsrc(cur.v, 2), nxt, none);
         int t = 2;
-        for (; t + 4 < ntiles; t += 2) {
+        for (; t + 2 < ntiles; t += 2) {
             step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(cur.k, t + 2), tile_rsrc(cur.v, t + 1), nxt, none);
             step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, none);
         }
-        // t = ntiles - 4: the next item's Q toward L2
-        step(C0{}, std::integral_constant<int, 1 | 4 | (FA_CHAIN_QPF ? 16 : 0)>{}, sa, sb, mx, tile_rsrc(cur.k, t + 2),
-             tile_rsrc(cur.v, t + 1), nxt, none);
-        step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, none);
-        t += 2;
         // t = ntiles - 2: K(t+2) = the next item's K(0) into K slot 0, V(t+1) ours; the next
         // Q^T loaded in phase B.  t = ntiles - 1: K(t+2) = next K(1) into slot 1, V(t+1) = next
-        // V(0) into slot 0; QK^T(next 0) -> sa
+        // V(0) into slot 0; QK^T(next 0) -> sa and its row max -> mx
         step(C0{}, std::integral_constant<int, 1 | 4 | 8>{}, sa, sb, mx, more ? tile_rsrc(nxt.k, 0) : none,
              tile_rsrc(cur.v, t + 1), nxt, none);
-        step(C1{}, std::integral_constant<int, 1 | 4 | 64>{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none,
-             more ? tile_rsrc(nxt.v, 0) : none, nxt, none);
+        step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none, more ? tile_rsrc(nxt.v, 0) : none, nxt,
+             none);
         // this item's O stays in the registers until the next item's step 0 stores it
         einv[0] = 1.f / rs[0][0];
         einv[1] = 1.f / rs[1][0];
-        m[0] = mx[0] + kM0;
-        m[1] = mx[1] + kM0;
+        m[0] = mx[0];
+        m[1] = mx[1];
         prev_o = o_rsrc(cur);
         if (!more) break;
         cur = nxt;

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--acc", action="store_true", help="also report the error against fp32")
+    ap.add_argument("--all", action="store_true", help="print every round's time per library")
     ap.add_argument("--kvtpb", type=int, default=0, help="time fa_fwd_v2 with this kv_tiles_per_block")
     ap.add_argument("--bpw", type=int, default=0,
                     help="with --kvtpb: blocks_per_workgroup of fa_fwd_v2_ex (0 = the library's grouping)")
@@ -109,6 +110,8 @@ def main():
             acc = f"  vs_fp32 max {err.max().item():.2e} mean {err.mean().item():.2e}"
         print(f"{p}: median {med * 1e3:.1f} us  min {min(times[i]) * 1e3:.1f} us  "
               f"{flops / (med * 1e-3) / 1e12:.1f} TFLOP/s  maxdiff_vs_0 {diff:.2e}{acc}", flush=True)
+        if args.all:
+            print("   rounds:", " ".join(f"{t * 1e3:.1f}" for t in times[i]), flush=True)
 
 
 if __name__ == "__main__":

@@ -215,3 +215,26 @@ def test_fullsize_c5_splitkv_emulated_w8(gpu):
     ks, vs, os_ = pick(k), pick(v), pick(out_rows)
     ref = attention_fp64(qs.double().numpy(), ks.double().numpy(), vs.double().numpy())
     _gate(os_, ref, torch.bfloat16, label="fullsize C5 W=8 emulated (16 heads x 256 rows)")
+
+
+@pytest.mark.parametrize("B,H,L", [(4, 16, 1024), (5, 13, 1024), (64, 8, 256), (2, 17, 2048), (8, 33, 512)],
+                         ids=["512-items", "520-items-uneven", "ntiles4", "l2048-uneven", "l512-uneven"])
+def test_chain_kernel_shapes(gpu, B, H, L):
+    """The chained persistent d = 128 kernel (fa_fwd16_chain.hpp: at least as many query tiles as
+    a 2-per-CU grid, Lk a multiple of 128 and >= 256) on shapes around its launch conditions:
+    exactly one workgroup per query tile, uneven item lists, the shortest chain (4 tiles), a
+    partial item count per XCD group -- sampled heads (first and last included, every query tile
+    of each) against the fp64 oracle, and bitwise repeatable."""
+    from exploring_flash_attention_amd import ops
+    d = 128
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + H * 10 + L)
+    q, k, v = (torch.randn(B, H, L, d, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    o1 = ops.attention_v1(q, k, v)
+    o2 = ops.attention_v1(q, k, v)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    n = min(12, B * H)
+    idx = sorted({round(i * (B * H - 1) / (n - 1)) for i in range(n)})
+    pick = lambda t: t.reshape(B * H, L, d)[idx][None].cpu()
+    ref = attention_fp64(pick(q).double().numpy(), pick(k).double().numpy(), pick(v).double().numpy())
+    _gate(pick(o1), ref, torch.bfloat16)
