@@ -22,14 +22,16 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     // d = 128 without a key tail: the 16x16x32 kernel (fa_fwd16_kernel.hpp; C3 +5 %, C4 +3.4 %,
     // the C5 partial pass +9 % over this file's 32x32x16 kernel)
     if constexpr (D == 128) {
-        if constexpr (MODE == kFinal && std::is_same_v<T, PT> && FA_CHAIN) {
-            // whole query-tile chains: an even number of 64-key tiles and at least one query
-            // tile per workgroup of a 2-per-CU grid
+        if constexpr ((MODE == kFinal && std::is_same_v<T, PT>) || (MODE == kFused && std::is_same_v<PT, f16s_t>)) {
+            // whole chains of query tiles (final) or of (query tile, key block) items (fused,
+            // scaled fp16 partials): an even number >= 4 of 64-key tiles per item, whole query
+            // tiles, and at least one item per workgroup of a 2-per-CU grid
             const int64_t grid = 2 * (int64_t)device_cus() / 8 * 8;
-            if (a.Lk % 128 == 0 && a.Lk >= 256 && a.Lq % kBQ == 0 && a.nsplit == 1 && nblk >= grid && grid >= 8 &&
-                nblk < (int64_t)1 << 31) {
-                hipLaunchKernelGGL((fa_fwd16_chain_kernel<T>), dim3((unsigned)grid), dim3(kThreads), lds, s, a,
-                                   (int)nblk);
+            const int64_t kvi = MODE == kFused ? a.kv_per_split : a.Lk;
+            if (FA_CHAIN && kvi % 128 == 0 && kvi >= 256 && a.Lk % kvi == 0 && a.Lq % kBQ == 0 &&
+                (MODE == kFused || a.nsplit == 1) && nblk >= grid && grid >= 8 && nblk < (int64_t)1 << 31) {
+                hipLaunchKernelGGL((fa_fwd16_chain_kernel<T, MODE>), dim3((unsigned)grid), dim3(kThreads),
+                                   lds + (MODE == kFused ? 16 : 0), s, a, (int)nblk);
                 return hipGetLastError();
             }
         }

@@ -41,8 +41,15 @@
 
 namespace fa {
 
-template <typename T>
+// MODE kFinal: items are query tiles, O stored.  MODE kFused (split-KV, scaled fp16 partials in
+// fragment order, fa_fwd16_kernel.hpp's workspace and hand-off): items are (query tile, key
+// block) pairs in decode_item's order; an item's normalised partial and {lse, e} are stored
+// during the next item's step 0 (sc1), the hand-off (counter add) is issued in its step 1 and
+// the workgroup that arrives last at a tile combines its partials right after that step.
+template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, int nitems) {
+    static_assert(MODE == kFinal || MODE == kFused, "chain modes");
+    constexpr bool FUSED = MODE == kFused;
     using M = Mma<T>;
     using v8 = typename M::v8;
     constexpr int D = 128;
@@ -74,7 +81,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n16 = lane & 15, g = lane >> 4;
-    const int ntiles = (int)(a.Lk / kBK);
+    const int ntiles = (int)((FUSED ? (int64_t)a.kv_per_split : a.Lk) / kBK);
 
     // per-item addressing: (query tile, b*h) of item j of this workgroup
     struct Item {
@@ -83,6 +90,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         const unsigned short* q;  // first row of the query tile
         int64_t o_row0;           // element offset of the tile's first O row
         int64_t q_rows;
+        int64_t grp;              // bh * nqt + qt (fused: the tile's counter)
+        int64_t blk;              // fused: the partial block (split, b*h, query tile)
     };
     // (every field wave-uniform: readfirstlane keeps the loop-carried item in SGPRs -- a
     // descriptor the compiler cannot prove uniform becomes a waterfall loop around each DMA)
@@ -94,12 +103,22 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     };
     auto item = [&](int j) {
         const int w = __builtin_amdgcn_readfirstlane(gstart + l + nl * j);
-        const int qt = w % a.nqt;
-        const int64_t bh = w / a.nqt;
+        int qt, split;
+        int64_t bh;
+        if constexpr (FUSED) {
+            decode_item(a, w, qt, split, bh);
+        } else {
+            qt = w % a.nqt;
+            split = 0;
+            bh = w / a.nqt;
+        }
         const int64_t q0 = (int64_t)qt * kBQ;
+        const int64_t kv0 = (int64_t)split * a.kv_per_split;
         Item it;
-        it.k = uni((const unsigned short*)a.k + bh * a.Lk * D);
-        it.v = uni((const unsigned short*)a.v + bh * a.Lk * D);
+        it.k = uni((const unsigned short*)a.k + (bh * a.Lk + kv0) * D);
+        it.v = uni((const unsigned short*)a.v + (bh * a.Lk + kv0) * D);
+        it.grp = bh * a.nqt + qt;
+        it.blk = (int64_t)split * a.BH * a.nqt + it.grp;
         it.q = uni((const unsigned short*)a.q + (bh * a.Lq + q0) * D);
         it.o_row0 = (bh * a.Lq + q0) * D;
         it.q_rows = a.Lq - q0 < kBQ ? a.Lq - q0 : kBQ;
@@ -222,20 +241,130 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // (EPI): lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n]; dv blocks 2e and 2e+1 are
     // paired by one v_permlane16_swap per dword into a 16-byte row store (fa_fwd16_kernel.hpp)
     const int o_lane = (wid * 32 + n16) * ROWB + 2 * (16 * (g & 1) + 8 * (g >> 1));
-    float einv[NQB] = {0.f, 0.f};  // 1 / row sum of the item whose O is still in the registers
-    auto store_group = [&](auto g_c, __amdgpu_buffer_rsrc_t ors) {
+    float einv[NQB] = {0.f, 0.f};  // 1 / row sum (fused: times 2^-e) of the item whose O is still in the registers
+    float elsev[NQB] = {0.f, 0.f};  // fused: its lse (log2 units) and per-row scale exponent e
+    float eesc[NQB] = {0.f, 0.f};
+    // row group G = (query block G / 4, dv blocks 2 (G % 4), +1) of v * inv as 16-bit rows
+    auto store_rows = [&](auto g_c, const f32x4 (&v)[NDB], float inv, __amdgpu_buffer_rsrc_t ors) {
         constexpr int G = decltype(g_c)::value, QB = G / 4, E = G % 4;
-        const float inv = einv[QB];
-        const unsigned x0 = pack2<T>(o[2 * E][QB][0] * inv, o[2 * E][QB][1] * inv);
-        const unsigned x1 = pack2<T>(o[2 * E][QB][2] * inv, o[2 * E][QB][3] * inv);
-        const unsigned y0 = pack2<T>(o[2 * E + 1][QB][0] * inv, o[2 * E + 1][QB][1] * inv);
-        const unsigned y1 = pack2<T>(o[2 * E + 1][QB][2] * inv, o[2 * E + 1][QB][3] * inv);
+        const unsigned x0 = pack2<T>(v[2 * E][0] * inv, v[2 * E][1] * inv);
+        const unsigned x1 = pack2<T>(v[2 * E][2] * inv, v[2 * E][3] * inv);
+        const unsigned y0 = pack2<T>(v[2 * E + 1][0] * inv, v[2 * E + 1][1] * inv);
+        const unsigned y1 = pack2<T>(v[2 * E + 1][2] * inv, v[2 * E + 1][3] * inv);
         const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{s0[0], s1[0], s0[1], s1[1]}, ors,
                                                o_lane + QB * 16 * ROWB + E * 64, 0, 0);
     };
+    auto store_group = [&](auto g_c, __amdgpu_buffer_rsrc_t ors) {
+        constexpr int QB = decltype(g_c)::value / 4;
+        f32x4 v[NDB];
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) v[db] = o[db][QB];
+        store_rows(g_c, v, einv[QB], ors);
+    };
     auto o_rsrc = [&](const Item& it) { return make_rsrc(uni((const unsigned short*)a.o + it.o_row0), kBQ * ROWB); };
+
+    // fused: the workspace of fa_fwd16_kernel.hpp's kFused mode -- per (split, b*h, query tile)
+    // block the normalised partial (scaled fp16) in fragment order, lse and e per row
+    constexpr int SC1 = 16;      // cache-policy bit: sc1
+    constexpr int NF = NDB * NQB;  // fragments (4 values) per lane
+    constexpr int BLK = kBQ * D;   // partial elements per block
+    struct Epi {
+        __amdgpu_buffer_rsrc_t o, l, e;
+    };
+    auto epi_of = [&](int64_t blk) {
+        Epi ep;
+        ep.o = make_rsrc(uni((const unsigned short*)a.o + blk * BLK), (int64_t)BLK * 2);
+        ep.l = make_rsrc(a.lse + blk * kBQ, (int64_t)kBQ * 4);
+        ep.e = make_rsrc(a.esc + blk * kBQ, (int64_t)kBQ * 4);
+        return ep;
+    };
+    auto frag_off = [&](int f) { return ((wid * NF + f) * 64 + lane) * 8; };
+    auto lse_off = [&](int qb) { return (wid * 32 + 16 * qb + n16) * 4; };
+    auto part_store = [&](auto f_c, const Epi& ep) {  // fragment f = db * NQB + qb
+        constexpr int F = decltype(f_c)::value, DB = F / NQB, QB = F % NQB;
+        const f32x4 x = o[DB][QB] * einv[QB];
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2<_Float16>(x[0], x[1]), pack2<_Float16>(x[2], x[3])}, ep.o,
+                                              frag_off(F), 0, SC1);
+    };
+    auto lse_store = [&](const Epi& ep) {  // (the 4 lanes of a row store the same value)
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(elsev[qb]), ep.l, lse_off(qb), 0, SC1);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(eesc[qb]), ep.e, lse_off(qb), 0, SC1);
+        }
+    };
+    // fused: the item's partial is complete (O, row sums, m): its scale and lse
+    auto finish_partial = [&]() {
+        float mxa[NQB];
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            float mv = 0.f;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mv = fmax_nc(mv, __builtin_fabsf(o[db][qb][i]));
+            mxa[qb] = mv;
+        }
+        quad_max2(mxa[0], mxa[1], mxa[0], mxa[1]);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            const float lsum = rs[qb][0];
+            const float inv = 1.f / lsum;
+            const int e = __builtin_amdgcn_frexp_expf(mxa[qb] * inv);
+            eesc[qb] = (float)e;
+            einv[qb] = __builtin_amdgcn_ldexpf(inv, -e);
+            elsev[qb] = m[qb] + __builtin_amdgcn_logf(lsum);  // lse in log2 units: m + log2(l)
+        }
+    };
+    // fused: the last workgroup at a tile sums its splits' partials in split order 0, 1, ...
+    // (bitwise repeatable whoever is last; fa_fwd16_kernel.hpp's combine) and writes O
+    auto combine = [&](int64_t grp, int64_t o_row0) {
+        const int ns = a.nsplit;
+        auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
+        const __amdgpu_buffer_rsrc_t ofin = make_rsrc(uni((const unsigned short*)a.o_final + o_row0), kBQ * ROWB);
+        static_for<NQB>([&](auto qb_c) {
+            constexpr int QB = decltype(qb_c)::value;
+            float Mx = -INFINITY, E = -1000.f;
+            for (int sp = 0; sp < ns; ++sp) {
+                const Epi ep = epi_of(blk_of(sp));
+                Mx = fmaxf(Mx, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1)));
+                E = fmaxf(E, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1)));
+            }
+            f32x4 acc[NDB];
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
+            float wsum = 0.f;
+            for (int sp = 0; sp < ns; ++sp) {
+                const Epi ep = epi_of(blk_of(sp));
+                const float wgt = __builtin_amdgcn_exp2f(
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1)) - Mx);
+                const float es = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
+                const float wv = __builtin_amdgcn_ldexpf(wgt, (int)(es - E));
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const u32x2 u = __builtin_bit_cast(
+                        u32x2, __builtin_amdgcn_raw_buffer_load_b64(ep.o, frag_off(db * NQB + QB), 0, SC1));
+                    f32x4 r;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const unsigned wd = u[jj >> 1];
+                        r[jj] = (float)__builtin_bit_cast(_Float16, (unsigned short)((jj & 1) ? (wd >> 16) : (wd & 0xffff)));
+                    }
+                    acc[db] += wv * r;
+                }
+                wsum += wgt;
+            }
+            const float inv_w = 1.f / wsum;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[db][i] = __builtin_amdgcn_ldexpf(acc[db][i] * inv_w, (int)E);
+            static_for<4>([&](auto e_c) { store_rows(std::integral_constant<int, 4 * QB + decltype(e_c)::value>{}, acc, 1.f, ofin); });
+        });
+    };
+    int* const flag_lds = (int*)(smem + 4 * TILEB);  // fused: the last adder's verdict
 
     // One step of fa_fwd16_kernel.hpp (see there); what differs is only where the tiles come
     // from: krs / vrs describe the K tile fetched now (t+2, possibly the next item's 0 or 1)
@@ -244,17 +373,22 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // t+1 exists: QK^T, row max, V DMA), 4 DMAK (a K tile is fetched), 8 QNEXT (the next item's
     // Q^T is loaded in phase B, after phase A's last read of the current one, and the closing
     // barrier leaves those loads in flight), 32 EPI (step 0 of an item whose predecessor's O is
-    // still in the registers: phase A stores it, one 16-byte row store per even slot, and phase
-    // B's first P.V / row-sum MFMAs start from zero instead of accumulating).
+    // still in the registers: phase A stores it -- final: one 16-byte row store per even slot,
+    // fused: one partial fragment per slot and the {lse, e} pairs -- and phase B's first P.V /
+    // row-sum MFMAs start from zero instead of accumulating), 128 HANDOFF (fused, step 1 of an
+    // item: if have_prev, one lane counts the previous item's block at its tile -- its stores
+    // were drained by step 0's barrier -- and, behind this step's barrier, leaves in LDS whether
+    // it was the last).
     auto step = [&](auto par_c, auto flags_c, f32x4 (&sc)[NKB][NQB], f32x4 (&sn)[NKB][NQB], float (&mx)[NQB],
-                    __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt,
-                    __amdgpu_buffer_rsrc_t ors) {
+                    __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt, const Epi& ep,
+                    int64_t pgrp, bool have_prev) {
         constexpr int P = decltype(par_c)::value;
         constexpr int F = decltype(flags_c)::value;
         constexpr bool MORE = F & 1;
         constexpr bool DMAK = F & 4;
         constexpr bool QNEXT = F & 8;
         constexpr bool EPI = F & 32;
+        constexpr bool HANDOFF = FUSED && (F & 128);
         using SLN = std::integral_constant<int, 1 - P>;
         using SLC = std::integral_constant<int, P>;
         if (!EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
@@ -268,6 +402,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
             }
         }
+        unsigned old = 0;
+        if constexpr (HANDOFF)
+            if (have_prev && tid == 0)
+                old = __hip_atomic_fetch_add(a.counters + pgrp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const float nm0 = -m[0], nm1 = -m[1];
         char* const kdst = kring + P * TILEB + wid * DPW * 1024;
         char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
@@ -316,7 +454,11 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
             if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key step 0 packs
             if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
-            if constexpr (EPI && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ors);
+            if constexpr (EPI && !FUSED && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ep.o);
+            if constexpr (EPI && FUSED) {
+                part_store(std::integral_constant<int, S>{}, ep);
+                if constexpr (S == 0) lse_store(ep);
+            }
             if constexpr (MORE) fence();
         });
 
@@ -365,6 +507,13 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             }
             fence();
         });
+        if constexpr (HANDOFF) {
+            if (tid == 0) {
+                const int last = have_prev && old + 1 == (unsigned)a.nsplit;
+                if (last) a.counters[pgrp] = 0;  // leave the counter zero for the next launch
+                *flag_lds = last;
+            }
+        }
         if constexpr (QNEXT) {
             // the K / V pieces issued before the Q loads have landed (their 2 * DPW pieces are
             // older than the 8 Q loads); the Q loads stay in flight into the next step, whose
@@ -399,36 +548,65 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     using C1 = std::integral_constant<int, 1>;
     using STEADY = std::integral_constant<int, 1 | 4>;
     const __amdgpu_buffer_rsrc_t none = make_rsrc32(cur.k, 0);
-    __amdgpu_buffer_rsrc_t prev_o = none;  // O tile of the previous item
+    const Epi enone = {none, none, none};
+    Epi prev_ep = enone;  // where the previous item's O / partial goes
+    int64_t prev_grp = 0, prev_orow = 0;
     for (int j = 0;; ++j) {
         const bool more = j + 1 < nmine;
         const Item nxt = item(more ? j + 1 : j);
-        // t = 0, 1 (step 0 stores the previous item's O)
+        // t = 0, 1 (step 0 stores the previous item's O or partial, step 1 hands a partial off)
         step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
-             nxt, prev_o);
-        step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, 3), tile_rsrc(cur.v, 2), nxt, none);
+             nxt, prev_ep, prev_grp, false);
+        step(C1{}, std::integral_constant<int, 1 | 4 | 128>{}, sb, sa, mx, tile_rsrc(cur.k, 3), tile_rsrc(cur.v, 2),
+             nxt, enone, prev_grp, j > 0);
+        if constexpr (FUSED) {
+            if (j > 0 && __builtin_amdgcn_readfirstlane(*flag_lds)) combine(prev_grp, prev_orow);
+        }
         int t = 2;
         for (; t + 2 < ntiles; t += 2) {
-            step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(cur.k, t + 2), tile_rsrc(cur.v, t + 1), nxt, none);
-            step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, none);
+            step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(cur.k, t + 2), tile_rsrc(cur.v, t + 1), nxt, enone, 0, false);
+            step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, enone, 0, false);
         }
         // t = ntiles - 2: K(t+2) = the next item's K(0) into K slot 0, V(t+1) ours; the next
         // Q^T loaded in phase B.  t = ntiles - 1: K(t+2) = next K(1) into slot 1, V(t+1) = next
         // V(0) into slot 0; QK^T(next 0) -> sa and its row max -> mx
         step(C0{}, std::integral_constant<int, 1 | 4 | 8>{}, sa, sb, mx, more ? tile_rsrc(nxt.k, 0) : none,
-             tile_rsrc(cur.v, t + 1), nxt, none);
+             tile_rsrc(cur.v, t + 1), nxt, enone, 0, false);
         step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none, more ? tile_rsrc(nxt.v, 0) : none, nxt,
-             none);
+             enone, 0, false);
         // this item's O stays in the registers until the next item's step 0 stores it
-        einv[0] = 1.f / rs[0][0];
-        einv[1] = 1.f / rs[1][0];
+        if constexpr (FUSED) {
+            finish_partial();
+            prev_ep = epi_of(cur.blk);
+        } else {
+            einv[0] = 1.f / rs[0][0];
+            einv[1] = 1.f / rs[1][0];
+            prev_ep = Epi{o_rsrc(cur), none, none};
+        }
+        prev_grp = cur.grp;
+        prev_orow = cur.o_row0;
         m[0] = mx[0];
         m[1] = mx[1];
-        prev_o = o_rsrc(cur);
         if (!more) break;
         cur = nxt;
     }
-    static_for<8>([&](auto g_c) { store_group(g_c, prev_o); });
+    if constexpr (FUSED) {
+        // the last item's partial, its hand-off and (if last at its tile) the combine
+        static_for<NF>([&](auto f_c) { part_store(f_c, prev_ep); });
+        lse_store(prev_ep);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned old = __hip_atomic_fetch_add(a.counters + prev_grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old + 1 == (unsigned)a.nsplit;
+            if (last) a.counters[prev_grp] = 0;
+            *flag_lds = last;
+        }
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(*flag_lds)) combine(prev_grp, prev_orow);
+    } else {
+        static_for<8>([&](auto g_c) { store_group(g_c, prev_ep.o); });
+    }
 }
 
 }  // namespace fa
