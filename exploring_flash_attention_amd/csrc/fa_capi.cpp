@@ -377,11 +377,20 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
     if (int st = check_dtype(dtype, &e)) return st;
     if (!supported_d(d) && !wide_d(d))
         return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel", (long long)d);
-    if (wide_d(d)) {  // the d-tiled kernels: 64 query rows; K / V chunks of at most 128 columns
-        if (bq) *bq = fa::dtiled_rows_per_block();
+    if (wide_d(d)) {  // the d-tiled kernels: 64 query rows, K / V chunks of at most 128 columns;
+                      // d = 384 16-bit: 128 rows, whole K / V tiles (the pair kernel)
+        if (e == fa::Elem::F64) {
+            if (bq) *bq = fa::dtiled_rows_per_block();
+            if (threads) *threads = fa::kThreads;
+            if (lds_bytes) *lds_bytes = (64 + 2 * 16) * 129 * 8 + 4 * 16 * 17 * 8;
+        } else {
+            int r = 0, th = 0, lds = 0;
+            fa::dtiled_geometry(e, (int)d, &r, &th, &lds);
+            if (bq) *bq = r;
+            if (threads) *threads = th;
+            if (lds_bytes) *lds_bytes = lds;
+        }
         if (bk) *bk = keys_per_tile(e, d);
-        if (threads) *threads = fa::kThreads;
-        if (lds_bytes) *lds_bytes = e == fa::Elem::F64 ? (64 + 2 * 16) * 129 * 8 + 4 * 16 * 17 * 8 : fa::dtiled_lds_bytes((int)d);
         return ok();
     }
     if (bq) *bq = fa::kBQ;

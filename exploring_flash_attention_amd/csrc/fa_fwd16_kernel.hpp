@@ -34,21 +34,6 @@
 
 namespace fa {
 
-// Row max of both query blocks at once: x0 (query n) and x1 (query 16 + n) are per-lane partial
-// maxima; the result is the max over the 4 lanes n, n+16, n+32, n+48 of each, in every lane.
-// Three swaps for the pair (a quad reduction per value would take four and two copies):
-// swap16(x0, x1) leaves rows 0 / 2 reducing x0 and rows 1 / 3 reducing x1 (one row = 16 lanes),
-// swap32 finishes both, and a last swap16 hands each lane both totals.
-__device__ __forceinline__ void quad_max2(float x0, float x1, float& m0, float& m1) {
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
-    const float y = fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
-    const float z = fmax_nc(__uint_as_float(s[0]), __uint_as_float(s[1]));
-    auto u = __builtin_amdgcn_permlane16_swap(__float_as_uint(z), __float_as_uint(z), false, false);
-    m0 = __uint_as_float(u[0]);
-    m1 = __uint_as_float(u[1]);
-}
-
 template <typename X> struct TypeTag { using type = X; };
 
 

@@ -14,4 +14,9 @@ __attribute__((weak)) hipError_t launch_fwd_dtiled(Elem, int, const FwdArgs&, hi
 hipError_t launch_fwd64_dtiled(int, const FwdArgs&, hipStream_t) { return hipErrorInvalidValue; }
 __attribute__((weak)) int dtiled_rows_per_block() { return 64; }
 __attribute__((weak)) int dtiled_lds_bytes(int d) { return (d <= 384 ? 3 : 4) * 16384; }
+__attribute__((weak)) void dtiled_geometry(Elem, int d, int* rows, int* threads, int* lds) {
+    *rows = 64;
+    *threads = 256;
+    *lds = dtiled_lds_bytes(d);
+}
 }  // namespace fa
