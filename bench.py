@@ -227,11 +227,20 @@ def time_step(torch, step, steps, warmup, barrier):
     return wall, ev0.elapsed_time(ev1)
 
 
-def fwd_kernel_name(d, Lk, what):
+def fwd_kernel_name(d, Lk, what, items=None, cus=256):
     """The kernel a contiguous forward launch runs (fa_fwd.hip launch_one): d = 128 with whole
-    64-key tiles on fa_fwd16_kernel (16x16x32 MFMA), everything else on fa_fwd_kernel."""
-    name = "fa_fwd16_kernel" if d == 128 and Lk % 64 == 0 else "fa_fwd_kernel"
+    128-key pairs of tiles and at least a query tile (item) per workgroup of a 2-per-CU grid on
+    fa_fwd16_chain_kernel (the chained persistent grid), other whole 64-key tiles at d = 128 on
+    fa_fwd16_kernel (16x16x32 MFMA), everything else on fa_fwd_kernel."""
+    if d == 128 and Lk % 128 == 0 and Lk >= 256 and items is not None and items >= 2 * cus:
+        name = "fa_fwd16_chain_kernel"
+    else:
+        name = "fa_fwd16_kernel" if d == 128 and Lk % 64 == 0 else "fa_fwd_kernel"
     return f"{name} ({what})"
+
+
+def _cus(torch):
+    return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
 
 
 def clock_settle(torch, step, seconds):
@@ -569,7 +578,7 @@ def main():
         if cfg["variant"] == "v1":
             def step():
                 ops.attention_v1(q, k, v, out=out)
-            kernel = fwd_kernel_name(d, L, "final")
+            kernel = fwd_kernel_name(d, L, "final", items=B * H * (L // 128), cus=_cus(torch))
         else:
             nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -577,9 +586,11 @@ def main():
             def step():
                 ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
             _, _, ppt = ops.v2_split_plan(B, H, L, d, cfg["kvtpb"], q.dtype)
-            kernel = (fwd_kernel_name(d, L, "fused split-KV, in-kernel combine") if ppt > 1
+            kernel = (fwd_kernel_name(d, L, "fused split-KV, in-kernel combine", items=B * H * (L // 128) * ppt,
+                                      cus=_cus(torch)) if ppt > 1
                       else fwd_kernel_name(d, L, "final: the library groups every key block of a query tile "
-                                                 "on one workgroup, fa_fwd_v2_split_plan"))
+                                                 "on one workgroup, fa_fwd_v2_split_plan",
+                                           items=B * H * (L // 128), cus=_cus(torch)))
         # Clock settle, immediately before the headline's --warmup (after the extras, whose
         # last shapes are small): the chip needs ~50 ms of back-to-back work before its clock
         # holds, so the headline's own step runs untimed for

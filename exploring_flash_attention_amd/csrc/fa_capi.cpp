@@ -377,8 +377,7 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
     if (int st = check_dtype(dtype, &e)) return st;
     if (!supported_d(d) && !wide_d(d))
         return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel", (long long)d);
-    if (wide_d(d)) {  // the d-tiled kernels: 64 query rows, K / V chunks of at most 128 columns;
-                      // d = 384 16-bit: 128 rows, whole K / V tiles (the pair kernel)
+    if (wide_d(d)) {  // the d-tiled kernels: 64 query rows, K / V chunks of at most 128 columns
         if (e == fa::Elem::F64) {
             if (bq) *bq = fa::dtiled_rows_per_block();
             if (threads) *threads = fa::kThreads;

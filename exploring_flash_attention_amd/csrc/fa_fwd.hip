@@ -23,15 +23,17 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
     // the C5 partial pass +9 % over this file's 32x32x16 kernel)
     if constexpr (D == 128) {
         if constexpr ((MODE == kFinal && std::is_same_v<T, PT>) || (MODE == kFused && std::is_same_v<PT, f16s_t>)) {
-            // whole chains of query tiles (final) or of (query tile, key block) items (fused,
-            // scaled fp16 partials): an even number >= 4 of 64-key tiles per item, whole query
-            // tiles, and at least one item per workgroup of a 2-per-CU grid
+            // whole chains of query tiles (final), or of the key blocks of query tiles (fused,
+            // scaled fp16 partials, each tile combined by its own workgroup): an even number >= 4
+            // of 64-key tiles per key block, whole query tiles, and at least one query tile per
+            // workgroup of a 2-per-CU grid
             const int64_t grid = 2 * (int64_t)device_cus() / 8 * 8;
             const int64_t kvi = MODE == kFused ? a.kv_per_split : a.Lk;
+            const int64_t tiles = (int64_t)a.nqt * a.BH;
             if (FA_CHAIN && kvi % 128 == 0 && kvi >= 256 && a.Lk % kvi == 0 && a.Lq % kBQ == 0 &&
-                (MODE == kFused || a.nsplit == 1) && nblk >= grid && grid >= 8 && nblk < (int64_t)1 << 31) {
+                (MODE == kFused || a.nsplit == 1) && tiles >= grid && grid >= 8 && nblk < (int64_t)1 << 31) {
                 hipLaunchKernelGGL((fa_fwd16_chain_kernel<T, MODE>), dim3((unsigned)grid), dim3(kThreads),
-                                   lds + (MODE == kFused ? 16 : 0), s, a, (int)nblk);
+                                   lds, s, a, (int)tiles);
                 return hipGetLastError();
             }
         }

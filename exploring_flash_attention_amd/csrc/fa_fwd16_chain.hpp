@@ -32,9 +32,9 @@
 // priority; it measured within noise), the next Q pulled toward L2 a few steps before the
 // seam (within noise), a lazy row max tested on the packed P bits (spilled, 3x slower).
 //
-// Requirements (checked by the launcher): contiguous [B, H, L, d], d = 128, Lk a multiple of
-// 128 of at least 256 (an even number >= 4 of 64-key tiles, so every item starts on ring
-// parity 0 and its first and last step pairs differ), Lq a multiple of 128 (every O row of a
+// Requirements (checked by the launcher): contiguous [B, H, L, d], d = 128, Lk (fused: keys per
+// block) a multiple of 128 of at least 256 (an even number >= 4 of 64-key tiles, so every item
+// starts on ring parity 0 and its first and last step pairs differ), Lq a multiple of 128 (every O row of a
 // tile exists: the stores need no row test), at least as many query tiles as workgroups.
 #pragma once
 #include "fa_fwd16_kernel.hpp"
@@ -42,10 +42,15 @@
 namespace fa {
 
 // MODE kFinal: items are query tiles, O stored.  MODE kFused (split-KV, scaled fp16 partials in
-// fragment order, fa_fwd16_kernel.hpp's workspace and hand-off): items are (query tile, key
-// block) pairs in decode_item's order; an item's normalised partial and {lse, e} are stored
-// during the next item's step 0 (sc1), the hand-off (counter add) is issued in its step 1 and
-// the workgroup that arrives last at a tile combines its partials right after that step.
+// fragment order, fa_fwd16_kernel.hpp's workspace): items are query tiles too, and a workgroup
+// walks an item's key blocks in order as one chain (block s's normalised partial and {lse, e}
+// stored during block s+1's step 0), then combines the tile's partials itself -- no counters,
+// no hand-off, the combine with the registers free.  Measured against the one-shot fused
+// kernel (outputs bitwise equal; profiles/r05/ab): B2 H2 L16384 at 16 partials 545 -> 503 us,
+// B1 H8 L16384 1061 -> 991 us, C4 at 4 partials 2120 -> 2044 us, C4 at 16 (the reference's one
+// block per workgroup) 3285 -> 3002 us.  The first version -- (tile, block) items chained in
+// decode order with the last arriver combining in the middle of its chain -- lost 4-10x: the
+// combine's serial loads under full register pressure.
 template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, int nitems) {
     static_assert(MODE == kFinal || MODE == kFused, "chain modes");
@@ -101,27 +106,27 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         const uint64_t hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
         return (const unsigned short*)(size_t)(lo | (hi << 32));
     };
-    auto item = [&](int j) {
+    auto item = [&](int j) {  // query tile w of this workgroup's list (fused: its split 0)
         const int w = __builtin_amdgcn_readfirstlane(gstart + l + nl * j);
-        int qt, split;
-        int64_t bh;
-        if constexpr (FUSED) {
-            decode_item(a, w, qt, split, bh);
-        } else {
-            qt = w % a.nqt;
-            split = 0;
-            bh = w / a.nqt;
-        }
+        const int qt = w % a.nqt;
+        const int64_t bh = w / a.nqt;
         const int64_t q0 = (int64_t)qt * kBQ;
-        const int64_t kv0 = (int64_t)split * a.kv_per_split;
         Item it;
-        it.k = uni((const unsigned short*)a.k + (bh * a.Lk + kv0) * D);
-        it.v = uni((const unsigned short*)a.v + (bh * a.Lk + kv0) * D);
+        it.k = uni((const unsigned short*)a.k + bh * a.Lk * D);
+        it.v = uni((const unsigned short*)a.v + bh * a.Lk * D);
         it.grp = bh * a.nqt + qt;
-        it.blk = (int64_t)split * a.BH * a.nqt + it.grp;
+        it.blk = it.grp;
         it.q = uni((const unsigned short*)a.q + (bh * a.Lq + q0) * D);
         it.o_row0 = (bh * a.Lq + q0) * D;
         it.q_rows = a.Lq - q0 < kBQ ? a.Lq - q0 : kBQ;
+        return it;
+    };
+    auto split_of = [&](const Item& t0, int sp) {  // fused: key block sp of the same query tile
+        Item it = t0;
+        const int64_t kv0 = (int64_t)sp * a.kv_per_split * D;
+        it.k = uni(t0.k + kv0);
+        it.v = uni(t0.v + kv0);
+        it.blk = (int64_t)sp * a.BH * a.nqt + t0.grp;
         return it;
     };
 
@@ -318,43 +323,67 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             elsev[qb] = m[qb] + __builtin_amdgcn_logf(lsum);  // lse in log2 units: m + log2(l)
         }
     };
-    // fused: the last workgroup at a tile sums its splits' partials in split order 0, 1, ...
-    // (bitwise repeatable whoever is last; fa_fwd16_kernel.hpp's combine) and writes O
+    // fused: the tile's partials summed in split order 0, 1, ... (fa_fwd16_kernel.hpp's combine,
+    // the same order and arithmetic: bitwise the one-shot kernel's O) and O written
     auto combine = [&](int64_t grp, int64_t o_row0) {
         const int ns = a.nsplit;
         auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
         const __amdgpu_buffer_rsrc_t ofin = make_rsrc(uni((const unsigned short*)a.o_final + o_row0), kBQ * ROWB);
+        // (U key blocks' loads in flight at a time: the walk schedule runs this between tiles,
+        // where nothing hides its latency; an index past the last block re-reads the last one,
+        // harmless to the maxima and given weight 0 in the sums -- the same sums in the same
+        // order, as acc never holds -0)
+        constexpr int U = 4;
         static_for<NQB>([&](auto qb_c) {
             constexpr int QB = decltype(qb_c)::value;
             float Mx = -INFINITY, E = -1000.f;
-            for (int sp = 0; sp < ns; ++sp) {
-                const Epi ep = epi_of(blk_of(sp));
-                Mx = fmaxf(Mx, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1)));
-                E = fmaxf(E, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1)));
+            for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                float lv[U], ev[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const Epi ep = epi_of(blk_of(sp0 + u < ns ? sp0 + u : ns - 1));
+                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1));
+                    ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    Mx = fmaxf(Mx, lv[u]);
+                    E = fmaxf(E, ev[u]);
+                }
             }
             f32x4 acc[NDB];
 #pragma unroll
             for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
             float wsum = 0.f;
-            for (int sp = 0; sp < ns; ++sp) {
-                const Epi ep = epi_of(blk_of(sp));
-                const float wgt = __builtin_amdgcn_exp2f(
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1)) - Mx);
-                const float es = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
-                const float wv = __builtin_amdgcn_ldexpf(wgt, (int)(es - E));
+            for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                float lv[U], ev[U];
+                u32x2 pv[U][NDB];
 #pragma unroll
-                for (int db = 0; db < NDB; ++db) {
-                    const u32x2 u = __builtin_bit_cast(
-                        u32x2, __builtin_amdgcn_raw_buffer_load_b64(ep.o, frag_off(db * NQB + QB), 0, SC1));
-                    f32x4 r;
+                for (int u = 0; u < U; ++u) {
+                    const Epi ep = epi_of(blk_of(sp0 + u < ns ? sp0 + u : ns - 1));
+                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1));
+                    ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const unsigned wd = u[jj >> 1];
-                        r[jj] = (float)__builtin_bit_cast(_Float16, (unsigned short)((jj & 1) ? (wd >> 16) : (wd & 0xffff)));
-                    }
-                    acc[db] += wv * r;
+                    for (int db = 0; db < NDB; ++db)
+                        pv[u][db] = __builtin_bit_cast(
+                            u32x2, __builtin_amdgcn_raw_buffer_load_b64(ep.o, frag_off(db * NQB + QB), 0, SC1));
                 }
-                wsum += wgt;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const float wgt = sp0 + u < ns ? __builtin_amdgcn_exp2f(lv[u] - Mx) : 0.f;
+                    const float wv = __builtin_amdgcn_ldexpf(wgt, (int)(ev[u] - E));
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db) {
+                        f32x4 r;
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            const unsigned wd = pv[u][db][jj >> 1];
+                            r[jj] = (float)__builtin_bit_cast(_Float16, (unsigned short)((jj & 1) ? (wd >> 16) : (wd & 0xffff)));
+                        }
+                        acc[db] += wv * r;
+                    }
+                    wsum += wgt;
+                }
             }
             const float inv_w = 1.f / wsum;
 #pragma unroll
@@ -364,7 +393,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             static_for<4>([&](auto e_c) { store_rows(std::integral_constant<int, 4 * QB + decltype(e_c)::value>{}, acc, 1.f, ofin); });
         });
     };
-    int* const flag_lds = (int*)(smem + 4 * TILEB);  // fused: the last adder's verdict
 
     // One step of fa_fwd16_kernel.hpp (see there); what differs is only where the tiles come
     // from: krs / vrs describe the K tile fetched now (t+2, possibly the next item's 0 or 1)
@@ -375,20 +403,15 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // barrier leaves those loads in flight), 32 EPI (step 0 of an item whose predecessor's O is
     // still in the registers: phase A stores it -- final: one 16-byte row store per even slot,
     // fused: one partial fragment per slot and the {lse, e} pairs -- and phase B's first P.V /
-    // row-sum MFMAs start from zero instead of accumulating), 128 HANDOFF (fused, step 1 of an
-    // item: if have_prev, one lane counts the previous item's block at its tile -- its stores
-    // were drained by step 0's barrier -- and, behind this step's barrier, leaves in LDS whether
-    // it was the last).
+    // row-sum MFMAs start from zero instead of accumulating).
     auto step = [&](auto par_c, auto flags_c, f32x4 (&sc)[NKB][NQB], f32x4 (&sn)[NKB][NQB], float (&mx)[NQB],
-                    __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt, const Epi& ep,
-                    int64_t pgrp, bool have_prev) {
+                    __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt, const Epi& ep) {
         constexpr int P = decltype(par_c)::value;
         constexpr int F = decltype(flags_c)::value;
         constexpr bool MORE = F & 1;
         constexpr bool DMAK = F & 4;
         constexpr bool QNEXT = F & 8;
         constexpr bool EPI = F & 32;
-        constexpr bool HANDOFF = FUSED && (F & 128);
         using SLN = std::integral_constant<int, 1 - P>;
         using SLC = std::integral_constant<int, P>;
         if (!EPI && __builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
@@ -402,10 +425,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
             }
         }
-        unsigned old = 0;
-        if constexpr (HANDOFF)
-            if (have_prev && tid == 0)
-                old = __hip_atomic_fetch_add(a.counters + pgrp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const float nm0 = -m[0], nm1 = -m[1];
         char* const kdst = kring + P * TILEB + wid * DPW * 1024;
         char* const vdst = vring + (1 - P) * TILEB + wid * DPW * 1024;
@@ -507,13 +526,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             }
             fence();
         });
-        if constexpr (HANDOFF) {
-            if (tid == 0) {
-                const int last = have_prev && old + 1 == (unsigned)a.nsplit;
-                if (last) a.counters[pgrp] = 0;  // leave the counter zero for the next launch
-                *flag_lds = last;
-            }
-        }
         if constexpr (QNEXT) {
             // the K / V pieces issued before the Q loads have landed (their 2 * DPW pieces are
             // older than the 8 Q loads); the Q loads stay in flight into the next step, whose
@@ -525,87 +537,107 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         }
     };
 
-    // prologue of the first item (fa_fwd16_kernel.hpp's)
-    Item cur = item(0);
-    load_q(cur);
-    dma_tile(cur.k, kring, 0);
-    dma_tile(cur.v, vring, 0);
-    dma_tile(cur.k, kring + TILEB, 1);
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[qb][ks]));
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPW) : "memory");
+    // prologue of an item's first tile (fa_fwd16_kernel.hpp's): Q, K(0), V(0), K(1); S(0)
     f32x4 sa[NKB][NQB], sb[NKB][NQB];
     float mx[NQB];
-    qk_all(std::integral_constant<int, 0>{}, sa);
-    rowmax_all(sa, mx);
-    m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
-    m[1] = mx[1];
-    __syncthreads();
+    auto prologue = [&](const Item& it) {
+        load_q(it);
+        dma_tile(it.k, kring, 0);
+        dma_tile(it.v, vring, 0);
+        dma_tile(it.k, kring + TILEB, 1);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[qb][ks]));
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * DPW) : "memory");
+        qk_all(std::integral_constant<int, 0>{}, sa);
+        rowmax_all(sa, mx);
+        m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
+        m[1] = mx[1];
+        __syncthreads();
+    };
 
     using C0 = std::integral_constant<int, 0>;
     using C1 = std::integral_constant<int, 1>;
     using STEADY = std::integral_constant<int, 1 | 4>;
+    Item cur = item(0);
     const __amdgpu_buffer_rsrc_t none = make_rsrc32(cur.k, 0);
     const Epi enone = {none, none, none};
-    Epi prev_ep = enone;  // where the previous item's O / partial goes
-    int64_t prev_grp = 0, prev_orow = 0;
-    for (int j = 0;; ++j) {
-        const bool more = j + 1 < nmine;
-        const Item nxt = item(more ? j + 1 : j);
-        // t = 0, 1 (step 0 stores the previous item's O or partial, step 1 hands a partial off)
-        step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
-             nxt, prev_ep, prev_grp, false);
-        step(C1{}, std::integral_constant<int, 1 | 4 | 128>{}, sb, sa, mx, tile_rsrc(cur.k, 3), tile_rsrc(cur.v, 2),
-             nxt, enone, prev_grp, j > 0);
-        if constexpr (FUSED) {
-            if (j > 0 && __builtin_amdgcn_readfirstlane(*flag_lds)) combine(prev_grp, prev_orow);
-        }
-        int t = 2;
-        for (; t + 2 < ntiles; t += 2) {
-            step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(cur.k, t + 2), tile_rsrc(cur.v, t + 1), nxt, enone, 0, false);
-            step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, enone, 0, false);
-        }
-        // t = ntiles - 2: K(t+2) = the next item's K(0) into K slot 0, V(t+1) ours; the next
-        // Q^T loaded in phase B.  t = ntiles - 1: K(t+2) = next K(1) into slot 1, V(t+1) = next
-        // V(0) into slot 0; QK^T(next 0) -> sa and its row max -> mx
-        step(C0{}, std::integral_constant<int, 1 | 4 | 8>{}, sa, sb, mx, more ? tile_rsrc(nxt.k, 0) : none,
-             tile_rsrc(cur.v, t + 1), nxt, enone, 0, false);
-        step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none, more ? tile_rsrc(nxt.v, 0) : none, nxt,
-             enone, 0, false);
-        // this item's O stays in the registers until the next item's step 0 stores it
-        if constexpr (FUSED) {
-            finish_partial();
-            prev_ep = epi_of(cur.blk);
-        } else {
+
+    if constexpr (!FUSED) {
+        prologue(cur);
+        Epi prev_ep = enone;  // where the previous item's O goes
+        for (int j = 0;; ++j) {
+            const bool more = j + 1 < nmine;
+            const Item nxt = item(more ? j + 1 : j);
+            // t = 0, 1 (step 0 stores the previous item's O)
+            step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
+                 nxt, prev_ep);
+            step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, 3), tile_rsrc(cur.v, 2), nxt, enone);
+            int t = 2;
+            for (; t + 2 < ntiles; t += 2) {
+                step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(cur.k, t + 2), tile_rsrc(cur.v, t + 1), nxt, enone);
+                step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(cur.k, t + 3), tile_rsrc(cur.v, t + 2), nxt, enone);
+            }
+            // t = ntiles - 2: K(t+2) = the next item's K(0) into K slot 0, V(t+1) ours; the next
+            // Q^T loaded in phase B.  t = ntiles - 1: K(t+2) = next K(1) into slot 1, V(t+1) =
+            // next V(0) into slot 0; QK^T(next 0) -> sa and its row max -> mx
+            step(C0{}, std::integral_constant<int, 1 | 4 | 8>{}, sa, sb, mx, more ? tile_rsrc(nxt.k, 0) : none,
+                 tile_rsrc(cur.v, t + 1), nxt, enone);
+            step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nxt.k, 1) : none, more ? tile_rsrc(nxt.v, 0) : none,
+                 nxt, enone);
+            // this item's O stays in the registers until the next item's step 0 stores it
             einv[0] = 1.f / rs[0][0];
             einv[1] = 1.f / rs[1][0];
             prev_ep = Epi{o_rsrc(cur), none, none};
+            m[0] = mx[0];
+            m[1] = mx[1];
+            if (!more) break;
+            cur = nxt;
         }
-        prev_grp = cur.grp;
-        prev_orow = cur.o_row0;
-        m[0] = mx[0];
-        m[1] = mx[1];
-        if (!more) break;
-        cur = nxt;
-    }
-    if constexpr (FUSED) {
-        // the last item's partial, its hand-off and (if last at its tile) the combine
-        static_for<NF>([&](auto f_c) { part_store(f_c, prev_ep); });
-        lse_store(prev_ep);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            const unsigned old = __hip_atomic_fetch_add(a.counters + prev_grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old + 1 == (unsigned)a.nsplit;
-            if (last) a.counters[prev_grp] = 0;
-            *flag_lds = last;
-        }
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(*flag_lds)) combine(prev_grp, prev_orow);
-    } else {
         static_for<8>([&](auto g_c) { store_group(g_c, prev_ep.o); });
+    } else {
+        // Split-KV, the reference's layout (one partial per key block in the workspace,
+        // flash_attention_v2/CUDA/flash_attention_v2.h:243-341): a workgroup walks the key blocks
+        // of its query tiles in order, chained like the final mode's items (block s's partial is
+        // stored while block s+1's first step runs), and combines the tile's partials itself
+        // once the last one is out -- its own stores, so no counter and no hand-off; the combine
+        // runs with the registers free (between tiles), not inside the chain.
+        const int ns = a.nsplit;
+        for (int j = 0; j < nmine; ++j) {
+            const Item t0 = j == 0 ? cur : item(j);
+            prologue(t0);
+            Epi prev_ep = enone;
+            for (int sp = 0;; ++sp) {
+                const bool more = sp + 1 < ns;
+                const Item it = split_of(t0, sp);
+                const Item nx = split_of(t0, more ? sp + 1 : sp);
+                step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(it.k, 2), tile_rsrc(it.v, 1),
+                     nx, prev_ep);
+                step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(it.k, 3), tile_rsrc(it.v, 2), nx, enone);
+                int t = 2;
+                for (; t + 2 < ntiles; t += 2) {
+                    step(C0{}, STEADY{}, sa, sb, mx, tile_rsrc(it.k, t + 2), tile_rsrc(it.v, t + 1), nx, enone);
+                    step(C1{}, STEADY{}, sb, sa, mx, tile_rsrc(it.k, t + 3), tile_rsrc(it.v, t + 2), nx, enone);
+                }
+                // the next block's K(0), K(1), V(0) (the same Q^T: no reload); after the last
+                // block empty ranges (zero tiles, an S(0) nobody reads)
+                step(C0{}, STEADY{}, sa, sb, mx, more ? tile_rsrc(nx.k, 0) : none, tile_rsrc(it.v, t + 1), nx, enone);
+                step(C1{}, STEADY{}, sb, sa, mx, more ? tile_rsrc(nx.k, 1) : none, more ? tile_rsrc(nx.v, 0) : none, nx,
+                     enone);
+                finish_partial();
+                prev_ep = epi_of(it.blk);
+                m[0] = mx[0];
+                m[1] = mx[1];
+                if (!more) break;
+            }
+            // the tile's last partial, then the combine (every wave's stores out first)
+            static_for<NF>([&](auto f_c) { part_store(f_c, prev_ep); });
+            lse_store(prev_ep);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            combine(t0.grp, t0.o_row0);
+        }
     }
 }
 

@@ -564,29 +564,54 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                 return r;
             }
         };
+        // U key blocks' loads in flight at a time (one at a time, the combine is a chain of
+        // memory latencies: the chained walk's C4 run went -10 % -> +9.5 % with this); an index
+        // past the last block re-reads the last one, harmless to the maxima and given weight 0 in
+        // the sums -- the same sums in the same order (acc never holds -0)
+        constexpr int U = sizeof(PT) == 4 ? 2 : 4;
+        auto clampsp = [&](int sp) { return sp < ns ? sp : ns - 1; };
 #pragma unroll
         for (int qb = 0; qb < NQB; ++qb) {
             float Mx = -INFINITY, E = -1000.f;
-            for (int sp = 0; sp < ns; ++sp) {
-                Mx = fmaxf(Mx, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1)));
-                if constexpr (SCALED)
-                    E = fmaxf(E, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1)));
+            for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                float lv[U], ev[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(clampsp(sp0 + u)), lse_off(qb), 0, SC1));
+                    if constexpr (SCALED)
+                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(clampsp(sp0 + u)), lse_off(qb), 0, SC1));
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    Mx = fmaxf(Mx, lv[u]);
+                    if constexpr (SCALED) E = fmaxf(E, ev[u]);
+                }
             }
             f32x4 acc[NDB];
 #pragma unroll
             for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
             float wsum = 0.f;
-            for (int sp = 0; sp < ns; ++sp) {
-                const float wgt = __builtin_amdgcn_exp2f(
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1)) - Mx);
-                float wv = wgt;
-                if constexpr (SCALED) {
-                    const float es = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
-                    wv = __builtin_amdgcn_ldexpf(wgt, (int)(es - E));
+            for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                float lv[U], ev[U];
+                f32x4 pv[U][NDB];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sp = clampsp(sp0 + u);
+                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1));
+                    if constexpr (SCALED)
+                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db) pv[u][db] = load_val(sp, db * NQB + qb);
                 }
 #pragma unroll
-                for (int db = 0; db < NDB; ++db) acc[db] += wv * load_val(sp, db * NQB + qb);
-                wsum += wgt;
+                for (int u = 0; u < U; ++u) {
+                    const float wgt = sp0 + u < ns ? __builtin_amdgcn_exp2f(lv[u] - Mx) : 0.f;
+                    float wv = wgt;
+                    if constexpr (SCALED) wv = __builtin_amdgcn_ldexpf(wgt, (int)(ev[u] - E));
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db) acc[db] += wv * pv[u][db];
+                    wsum += wgt;
+                }
             }
             float inv_w = 1.f / wsum;
             if constexpr (SCALED) {

@@ -61,7 +61,6 @@ constexpr int dt_slots(int d) {
 
 int dtiled_rows_per_block() { return kDtRows; }
 int dtiled_lds_bytes(int d) { return dt_slots(d) * kDtSlotB; }
-bool dtiled_pair(Elem e, int d);  // (below: d = 384 in bf16 / fp16 runs the pair kernel)
 
 // s_waitcnt vmcnt(N), N a compile-time count of DMA pieces allowed to stay in flight
 template <int N>
@@ -340,280 +339,11 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// d = 384 (round 5): 32 query rows per wave pair, the head dim split between the pair's two waves.
-//
-// The 16-row kernel above reads the whole K and V tile from LDS per 16 query rows (1.47 LDS
-// instructions per MFMA at d = 384, against 0.71 in the d = 128 kernel) and passes a 4-wave barrier
-// every 16 MFMAs per wave.  Here a workgroup of 8 waves serves 128 rows: pair p (waves p and p + 4,
-// the same SIMD under the cyclic wave placement) owns rows 32p .. 32p + 31, and wave half h = 0 / 1
-// of the pair owns head-dim columns [192h, 192h + 192): its Q^T half (48 VGPRs) and its O^T half
-// (96 VGPRs).  Per 64-key tile:
-//   * QK^T over the wave's 6 k-steps (each K fragment feeds both 16-query blocks), the partial S
-//     written to LDS (8 KiB per wave), a barrier, the partner's partial read and added -- IEEE
-//     addition commutes, so both waves hold bit-identical S = S_0 + S_1 -- and the online softmax
-//     computed by both waves (identical m, P and row sums);
-//   * P.V for the wave's 12 dv blocks.
-// The whole K and V tiles stay in LDS (48 KiB each) beside the S exchange (64 KiB): 160 KiB, one
-// workgroup per CU (two waves per SIMD).  Two barriers per tile: B1 after the S writes (K(t) free:
-// K(t+1) is DMA'd; V(t) landed: every wave waited for its pieces before it), B2 after P.V (V(t)
-// free: V(t+1) is DMA'd; K(t+1) landed).  LDS read traffic per MFMA is 2/3 of the 16-row kernel's,
-// and a barrier comes every ~50 MFMAs per wave instead of 16.  The d tiles of the reference
-// launcher are validated by the C ABI; this kernel's QK^T sums its two halves' k-steps, so its bits
-// differ from the 16-row kernel's (both against the fp64 oracle at the bf16 gates) and do not
-// depend on the tiles.
-constexpr int kDpWaves = 8;
-constexpr int kDpRows = 128;
-int dpair_rows_per_block() { return kDpRows; }
-constexpr int kDpLds = 2 * 64 * 384 * 2 + kDpWaves * 8192;  // K + V tiles + S exchange = 160 KiB
-
-template <typename T>
-__global__ __launch_bounds__(kDpWaves * 64, 1) void fa_fwd_dp384_kernel(FwdArgs a) {
-    using M = Mma<T>;
-    using v8 = typename M::v8;
-    constexpr int D = 384, HALF = 192;
-    constexpr int ROWB = 2 * D;        // bytes per K / V row (global and LDS image)
-    constexpr int TILEB = 64 * ROWB;   // one K or V tile image
-    constexpr int NKSH = HALF / 32;    // QK^T k-steps per half
-    constexpr int NDBH = HALF / 16;    // O^T column blocks per half
-    constexpr int NKB = 4, NQB = 2;
-    constexpr int PPW = TILEB / 1024 / kDpWaves;  // DMA pieces per wave per tile (6)
-    static_assert(PPW * 1024 * kDpWaves == TILEB, "pieces");
-
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* const kimg = smem;
-    char* const vimg = smem + TILEB;
-    char* const sx = smem + 2 * TILEB;  // S exchange: 8 KiB per wave
-
-    const int nqt = (int)((a.Lq + kDpRows - 1) / kDpRows);
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const int qt = w % nqt;
-    const int64_t bh = w / nqt;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int pr = wid & 3, h = wid >> 2;  // pair, half
-    const int n16 = lane & 15, g = lane >> 4;
-    const int nkv = (int)a.Lk;
-    const int ntiles = (nkv + 63) / 64;
-
-    // Q^T half fragments: lane (g, n) holds Q[32 pr + 16 qb + n][192 h + 32 ks + 8 pg .. +7]
-    const int pg = (0x2130 >> (4 * g)) & 3;
-    const int64_t q_tile0 = (int64_t)qt * kDpRows;
-    const unsigned short* Qh = (const unsigned short*)a.q + (bh * a.Lq + q_tile0) * D;
-    const int64_t q_rows = a.Lq - q_tile0 < kDpRows ? a.Lq - q_tile0 : kDpRows;
-    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, q_rows * ROWB);
-    v8 qf[NQB][NKSH];
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-        for (int ks = 0; ks < NKSH; ++ks)
-            qf[qb][ks] = __builtin_bit_cast(v8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    qrs, (32 * pr + 16 * qb + n16) * ROWB + 2 * HALF * h + ks * 64 + pg * 16, 0, 0));
-
-    // LDS-DMA of a whole tile: image byte b <- source row / 16-byte chunk of the swizzled
-    // subtile image (8 rows x 32 columns, 512 B; rows of ROWB bytes)
-    const char* const kbase = (const char*)a.k + bh * a.Lk * ROWB;
-    const char* const vbase = (const char*)a.v + bh * a.Lk * ROWB;
-    int src[PPW];
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-        const int b = (wid * PPW + i) * 1024 + lane * 16;
-        const int rg = b / (8 * ROWB), rem = b % (8 * ROWB);
-        const int row = 8 * rg + (rem % 512) / 64;
-        const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
-        src[i] = row * ROWB + ch * 16;
-    }
-    auto dma = [&](const char* base, char* img, int t) {
-        const int valid = nkv - t * 64 < 64 ? nkv - t * 64 : 64;  // rows past the last key read zeros
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc32(base + (int64_t)t * TILEB, valid * ROWB);
-#pragma unroll
-        for (int i = 0; i < PPW; ++i) dma16_asm(rs, img + (wid * PPW + i) * 1024, src[i]);
-    };
-
-    // LDS read geometry (fa_fwd16_kernel.hpp): K rows in the order rho(n), V^T by transposed reads
-    const int rho = 8 * ((n16 >> 2) & 1) + 4 * (n16 >> 3) + (n16 & 3);
-    const unsigned kl = (rho >> 3) * (8 * ROWB) + 64 * (rho & 7) + 16 * (pg ^ ((rho >> 2) & 3));
-    const int r0 = 8 * (g & 1) + 4 * (g >> 1) + (n16 >> 2);
-    const int sw = (r0 >> 2) & 3, c0 = (n16 >> 1) & 1;
-    const unsigned vrow = (r0 >> 3) * (8 * ROWB) + 64 * (r0 & 7) + 8 * (n16 & 1);
-    const unsigned vl_e = vrow + 16 * (c0 ^ sw), vl_o = vrow + 16 * ((2 + c0) ^ sw);
-    const int R0 = 8 * (g & 1) + 4 * (g >> 1);
-    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-    f32x4 o[NDBH][NQB];
-#pragma unroll
-    for (int db = 0; db < NDBH; ++db)
-#pragma unroll
-        for (int qb = 0; qb < NQB; ++qb) o[db][qb] = f32x4{};
-    f32x4 rs[NQB] = {f32x4{}, f32x4{}};
-    float m[NQB] = {-INFINITY, -INFINITY};
-    v8 ones;
-    {
-        constexpr unsigned kOne = std::is_same_v<T, __bf16> ? 0x3F80u : 0x3C00u;
-        ones = __builtin_bit_cast(v8, u32x4{kOne | (kOne << 16), kOne | (kOne << 16), kOne | (kOne << 16),
-                                            kOne | (kOne << 16)});
-    }
-    const float c = a.scale_log2;
-    char* const sx_own = sx + wid * 8192 + lane * 16;
-    char* const sx_par = sx + (wid ^ 4) * 8192 + lane * 16;
-
-    // prologue: K(0), V(0) (every DMA piece is inline asm: the compiler sees no LDS write)
-    dma(kbase, kimg, 0);
-    dma(vbase, vimg, 0);
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-        for (int ks = 0; ks < NKSH; ++ks) asm volatile("" : "+v"(qf[qb][ks]));
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-
-    for (int t = 0; t < ntiles; ++t) {
-        // ---- S^T half = K Q^T over this wave's 6 k-steps
-        f32x4 s[NKB][NQB];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) s[kb][qb] = f32x4{};
-#pragma unroll
-        for (int ks = 0; ks < NKSH; ++ks) {
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-                const u32x4 kf = *(const u32x4*)(kimg + kl + kb * 16 * ROWB + 512 * (NKSH * h + ks));
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb) s[kb][qb] = M::mma16(__builtin_bit_cast(v8, kf), qf[qb][ks], s[kb][qb]);
-            }
-        }
-        // ---- exchange the halves: own partial out, barrier B1, partner's in
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) *(f32x4*)(sx_own + (kb * NQB + qb) * 1024) = s[kb][qb];
-        // B1: every wave's S writes done and its V(t) pieces landed (V(t) is the only DMA in
-        // flight); after it K(t) is free -- K(t+1) goes out
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (t + 1 < ntiles) dma(kbase, kimg, t + 1);
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) s[kb][qb] += *(const f32x4*)(sx_par + (kb * NQB + qb) * 1024);
-        // keys past the end (last tile only): score -inf
-        if (nkv - t * 64 < 64) {
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (t * 64 + 16 * kb + R0 + i >= nkv) {
-                        s[kb][0][i] = -INFINITY;
-                        s[kb][1][i] = -INFINITY;
-                    }
-        }
-        // ---- online softmax (base 2), both waves of the pair on identical S
-        float mx[NQB];
-        {
-            float p0 = fmax_nc(fmax_nc(fmax_nc(s[0][0][0], s[0][0][1]), s[0][0][2]), s[0][0][3]);
-            float p1 = fmax_nc(fmax_nc(fmax_nc(s[0][1][0], s[0][1][1]), s[0][1][2]), s[0][1][3]);
-#pragma unroll
-            for (int kb = 1; kb < NKB; ++kb) {
-                p0 = fmax_nc(fmax_nc(fmax_nc(fmax_nc(p0, s[kb][0][0]), s[kb][0][1]), s[kb][0][2]), s[kb][0][3]);
-                p1 = fmax_nc(fmax_nc(fmax_nc(fmax_nc(p1, s[kb][1][0]), s[kb][1][1]), s[kb][1][2]), s[kb][1][3]);
-            }
-            quad_max2(p0, p1, mx[0], mx[1]);
-        }
-        float mn[NQB];
-#pragma unroll
-        for (int qb = 0; qb < NQB; ++qb) mn[qb] = fmaxf(m[qb], mx[qb] * c);
-        if (__builtin_amdgcn_ballot_w64(mn[0] > m[0] || mn[1] > m[1])) {
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) {
-                const float alpha = __builtin_amdgcn_exp2f(m[qb] - mn[qb]);  // 0 on the first tile
-                rs[qb] *= alpha;
-#pragma unroll
-                for (int db = 0; db < NDBH; ++db) o[db][qb] *= alpha;
-                m[qb] = mn[qb];
-            }
-        }
-        u32x4 pbu[2][NQB];  // P^T fragments of the two 32-key k-steps (fa_fwd16_kernel.hpp order)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int kb = 2 * kk + (j >> 1), i = 2 * (j & 1);
-                    pbu[kk][qb][j] = pack2<T>(__builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][qb][i], c, -m[qb])),
-                                              __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][qb][i + 1], c, -m[qb])));
-                }
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) rs[qb] = M::mma16(ones, __builtin_bit_cast(v8, pbu[kk][qb]), rs[qb]);
-        // ---- O^T half += V^T P^T over this wave's 12 dv blocks
-#pragma unroll
-        for (int db = 0; db < NDBH; ++db) {
-            const int gdb = NDBH * h + db;  // dv block in the tile image
-            const char* const vb = vimg + ((gdb & 1) ? vl_o : vl_e) + 512 * (gdb >> 1);
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                const u32x2 v0 = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                                              (lds_s16x4*)(vb + kk * 32 * ROWB)));
-                const u32x2 v1 = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                                              (lds_s16x4*)(vb + kk * 32 * ROWB + 16 * ROWB)));
-                const u32x4 vv = {v0[0], v0[1], v1[0], v1[1]};
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb)
-                    o[db][qb] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[kk][qb]), o[db][qb]);
-            }
-        }
-        // B2: every wave done with V(t) and with the S exchange; K(t+1) landed -- V(t+1) goes out
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (t + 1 < ntiles) dma(vbase, vimg, t + 1);
-    }
-
-    // ---- epilogue: lane (g, n) holds O^T[192 h + 16 db + 4 g + i][query 32 pr + 16 qb + n]
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb) {
-        const int64_t q_row = q_tile0 + 32 * pr + 16 * qb + n16;
-        if (q_row < a.Lq) {
-            const float inv = 1.f / rs[qb][0];
-            unsigned short* const Oh = (unsigned short*)a.o + (bh * a.Lq + q_row) * D + HALF * h;
-#pragma unroll
-            for (int e = 0; e < NDBH / 2; ++e) {
-                const unsigned x0 = pack2<T>(o[2 * e][qb][0] * inv, o[2 * e][qb][1] * inv);
-                const unsigned x1 = pack2<T>(o[2 * e][qb][2] * inv, o[2 * e][qb][3] * inv);
-                const unsigned y0 = pack2<T>(o[2 * e + 1][qb][0] * inv, o[2 * e + 1][qb][1] * inv);
-                const unsigned y1 = pack2<T>(o[2 * e + 1][qb][2] * inv, o[2 * e + 1][qb][3] * inv);
-                const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-                const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-                const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
-                *(u32x4*)(Oh + 32 * e + 16 * (g & 1) + 8 * (g >> 1)) = u;
-            }
-        }
-    }
-}
-
-#ifndef FA_DPAIR
-#define FA_DPAIR 1  // d = 384 (bf16 / fp16): the pair kernel instead of the 16-row chunked one
-#endif
-bool dtiled_pair(Elem e, int d) { return FA_DPAIR && d == 384 && (e == Elem::BF16 || e == Elem::F16); }
-void dtiled_geometry(Elem e, int d, int* rows, int* threads, int* lds) {
-    const bool p = dtiled_pair(e, d);
-    *rows = p ? kDpRows : kDtRows;
-    *threads = p ? kDpWaves * 64 : kDtWaves * 64;
-    *lds = p ? kDpLds : dtiled_lds_bytes(d);
-}
-
-template <typename T>
-static hipError_t launch_dp384(const FwdArgs& a, hipStream_t s) {
-    static bool attr_set = false;  // (160 KiB of dynamic LDS needs the attribute once)
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void*)fa_fwd_dp384_kernel<T>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kDpLds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    const int64_t nqt = (a.Lq + kDpRows - 1) / kDpRows;
-    hipLaunchKernelGGL((fa_fwd_dp384_kernel<T>), dim3((unsigned)(nqt * a.BH)), dim3(kDpWaves * 64), kDpLds, s, a);
-    return hipGetLastError();
+// the kernel geometry the C ABI reports for a wide head dim (fa_kernel_geometry)
+void dtiled_geometry(Elem, int d, int* rows, int* threads, int* lds) {
+    *rows = kDtRows;
+    *threads = kDtWaves * 64;
+    *lds = dtiled_lds_bytes(d);
 }
 
 template <typename T, int D>
@@ -642,10 +372,6 @@ static hipError_t launch_dt(const FwdArgs& a, const dim3& grid, int lds, hipStre
 hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
     const int lds = dtiled_lds_bytes(d);
-    if (dtiled_pair(t, d)) {
-        if (t == Elem::BF16) return launch_dp384<__bf16>(a, s);
-        if (t == Elem::F16) return launch_dp384<_Float16>(a, s);
-    }
     if (t == Elem::BF16) {
         if (d == 384) return launch_dt<__bf16, 384>(a, grid, lds, s);
         if (d == 512) return launch_dt<__bf16, 512>(a, grid, lds, s);

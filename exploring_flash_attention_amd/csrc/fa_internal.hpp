@@ -143,7 +143,6 @@ hipError_t launch_fwd64_dtiled(int d, const FwdArgs& a, hipStream_t s);
 int dtiled_rows_per_block();
 int dtiled_lds_bytes(int d);
 // the wide-d kernel serving (dtype, d): query rows per workgroup, threads, dynamic LDS bytes
-// (d = 384 in bf16 / fp16: the pair kernel, 128 rows, 512 threads, 160 KiB)
 void dtiled_geometry(Elem e, int d, int* rows, int* threads, int* lds);
 
 }  // namespace fa

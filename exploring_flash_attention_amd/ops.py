@@ -178,14 +178,20 @@ def attention_v1(q, k, v, out=None):
 
 
 def _d_tiles(d, d_tile_qk, d_tile_v):
-    """d tiles default to min(32, d) (the reference's D_TILE = 32 where d allows it)."""
-    return (min(32, d) if d_tile_qk is None else int(d_tile_qk),
-            min(32, d) if d_tile_v is None else int(d_tile_v))
+    """d tiles the caller left as None: min(32, d) up to d = 256 (the reference's D_TILE = 32
+    where d allows it; there the tiles are only validated -- one LDS tile holds a whole row),
+    128 above, where the d-tiled kernel streams K / V in tile-wide column chunks.  The output
+    is bitwise the same for every tile choice, only the speed differs: d = 512 B32 H8 L1024,
+    32/32 0.931 ms against 128/128 0.682 ms (24 chunk waits + barriers per 64-key tile against
+    6; gpurun_out/r05i/dtile_sweep.txt, profiles/r05/dtile_sweep.txt)."""
+    dflt = min(32, d) if d <= 256 else 128
+    return (dflt if d_tile_qk is None else int(d_tile_qk),
+            dflt if d_tile_v is None else int(d_tile_v))
 
 
 def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
     """FA-v1 d-tiled forward (O_acc in VGPRs); d tiles as in the reference launcher
-    (0 < d_tile <= d; default min(32, d)).  d <= 256: one LDS tile holds a whole row and the
+    (0 < d_tile <= d; default min(32, d) up to d = 256, 128 above -- see _d_tiles).  d <= 256: one LDS tile holds a whole row and the
     fused kernel runs (tiles validated); 256 < d <= 512: the d-tiled kernel streams K and V
     through LDS in d_tile-wide column chunks (rounded down to 32, 64 or 128 columns)."""
     _check_qkv(q, k, v, strided=True)

@@ -106,5 +106,8 @@ def test_kernel_labels_follow_the_dispatch():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.fwd_kernel_name(128, 1024, "final").startswith("fa_fwd16_kernel")
+    # C3: 2048 query tiles >= 2 x 256 CUs -> the chained persistent grid (fa_fwd.hip launch_one)
+    assert bench.fwd_kernel_name(128, 1024, "final", items=2048, cus=256).startswith("fa_fwd16_chain_kernel")
+    assert bench.fwd_kernel_name(128, 1024, "final", items=256, cus=256).startswith("fa_fwd16_kernel")
     assert bench.fwd_kernel_name(128, 1000, "final").startswith("fa_fwd_kernel")
     assert bench.fwd_kernel_name(32, 1024, "final").startswith("fa_fwd_kernel")

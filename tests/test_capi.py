@@ -55,8 +55,7 @@ def test_version_and_geometry():
         L.geometry(96)
     # the d-tiled kernels: 64 query rows, 64-key tiles, a ring of 16 KiB chunk images (8 slots
     # at d = 512: one workgroup per CU; 4 at d = 384: two)
-    # d = 384 16-bit: the pair kernel (128 rows, 8 waves, whole K / V tiles + the S exchange)
-    assert L.geometry(512) == (64, 64, 256, 4 * 16384) and L.geometry(384) == (128, 64, 512, 2 * 49152 + 8 * 8192)
+    assert L.geometry(512) == (64, 64, 256, 4 * 16384) and L.geometry(384) == (64, 64, 256, 3 * 16384)
     assert L.geometry(384, L.FA_DTYPE_FP64)[:3] == (64, 16, 256)
 
 
@@ -343,3 +342,14 @@ def test_dist_argument_and_error_paths():
     nbytes = ctypes.c_size_t()
     assert lib.fa_fwd_v2_dist_workspace_size(1, 1, 64, 128, 2, L.FA_DTYPE_FP64, L.FA_DTYPE_FP32,
                                              ctypes.byref(nbytes)) == L.FA_ERR_UNSUPPORTED
+
+
+def test_d_tile_defaults():
+    """None d tiles: min(32, d) up to d = 256 (the reference's D_TILE), 128 for the d-tiled
+    kernel's wide head dims (24 vs 6 chunk waits per key tile; the result is the same)."""
+    from exploring_flash_attention_amd import ops
+    assert ops._d_tiles(16, None, None) == (16, 16)
+    assert ops._d_tiles(128, None, None) == (32, 32)
+    assert ops._d_tiles(256, None, 64) == (32, 64)
+    assert ops._d_tiles(384, None, None) == (128, 128)
+    assert ops._d_tiles(512, 32, None) == (32, 128)

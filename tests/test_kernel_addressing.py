@@ -287,45 +287,6 @@ def test_dtiled_kernel_in_bounds(B, H, L, d, dq, dv):
     o.check(np.where(live, 2 * (bh[:, None] * L * D + rows * D), 0), np.where(live, ROWD, 0), "O row store")
 
 
-@pytest.mark.parametrize("B,H,L", [(32, 8, 1024), (2, 3, 200), (1, 2, 77), (1, 1, 1), (3, 1, 129)])
-def test_dpair384_kernel_in_bounds(B, H, L):
-    """csrc/fa_fwd_dtiled.hip fa_fwd_dp384_kernel (d = 384, 16-bit): 128-row query tiles (pairs of
-    waves split the head dim); per 64-key tile the whole K / V tile is DMA'd through a descriptor
-    that ends at the last valid key's row; each wave stores its 192-column half of its 32 rows."""
-    BH, D, ROWD = B * H, 384, 768
-    nqt = -(-L // 128)
-    nblk = nqt * BH
-    w = xcd_remap(np.arange(nblk, dtype=np.int64), nblk)
-    assert np.array_equal(np.sort(w), np.arange(nblk))
-    qt, bh = w % nqt, w // nqt
-    q, k, v, o = (_tensor(n, B, H, L, D) for n in "qkvo")
-    q_tile0 = qt * 128
-    q_rows = np.minimum(L - q_tile0, 128)
-    q.check(2 * (bh * L * D + q_tile0 * D), q_rows * ROWD, "Q descriptor")
-    for t in range(-(-L // 64)):
-        valid = min(64, L - t * 64)
-        for alloc in (k, v):
-            alloc.check(bh * L * ROWD + t * 64 * ROWD, valid * ROWD, f"tile t={t}")
-    rows = q_tile0[:, None] + np.arange(128)[None, :]
-    live = rows < L
-    for h in (0, 1):  # each half-row store: 192 columns
-        o.check(np.where(live, 2 * (bh[:, None] * L * D + rows * D + 192 * h), 0), np.where(live, 384, 0),
-                "O half-row store")
-    # the LDS image: every byte of a tile image is written by exactly one lane of one piece, and
-    # each lane's source (row, 16-byte chunk) is the one the swizzled layout puts there
-    seen = np.zeros(64 * ROWD // 16, dtype=np.int64)
-    for wid in range(8):
-        for i in range(6):
-            for lane in range(64):
-                b = (wid * 6 + i) * 1024 + lane * 16
-                rg, rem = b // (8 * ROWD), b % (8 * ROWD)
-                row = 8 * rg + (rem % 512) // 64
-                ch = 4 * (rem // 512) + (((rem % 64) // 16) ^ ((row >> 2) & 3))
-                assert (row >> 3) * 8 * ROWD + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3)) == b
-                seen[b // 16] += 1
-    assert (seen == 1).all()
-
-
 def chain_items(nitems, grid):
     """fa_fwd16_chain.hpp's static schedule: block b serves XCD group b % 8 and takes items
     l, l + G/8, ... (l = b / 8) of the contiguous range xcd_remap gives the group."""
