@@ -11,7 +11,7 @@ mkdir -p $O
 timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- \
     python3 bench.py --gpus 1 --steps 500 --warmup 300 --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/bench.err
 rc=$?; echo "kernel stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
-for c in ${PMC_CONFIGS:-c3 b1h1l16k c4g1 c4g4 d384}; do
+for c in ${PMC_CONFIGS:-c3 b1h1l16k b2h2l16k c4g1 c4g4 d384 d512}; do
   for i in 1 2; do
     grp=$([ $i = 1 ] && echo FETCH_SIZE || echo WRITE_SIZE)
     timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc_$c/p$i -o run --output-format csv -- \

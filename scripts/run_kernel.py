@@ -7,7 +7,8 @@ c4g1 (C4 with 4 / 1 key blocks per workgroup: 4 / 16 partials per query tile), b
 shape the library splits itself: 4 partials per query tile since round 4's plan, 2 before),
 b1h2l16k (2 partials per tile; 1 before), b1h1l16k_unsplit (the same shape,
 one workgroup per query tile), b1h2l4k / _unsplit (4 partials per tile / none), c5 (one rank's
-C5 partial kernel shape, FA-v1 form), d384 / d512 (the d-tiled kernel at B32 H8 L1024).
+C5 partial kernel shape, FA-v1 form), b2h2l16k (16 partials per tile: the fused chain's walk),
+d384 / d512 (the d-tiled kernel at B32 H8 L1024).
 """
 import os
 import sys
@@ -23,6 +24,7 @@ CFG = {"c2": (32, 8, 1024, 32, "v1", None), "c3": (32, 8, 1024, 128, "v1", None)
        "b1h1l16k_unsplit": (1, 1, 16384, 128, "v2", 64),
        "b1h2l16k": (1, 2, 16384, 128, "v2", None), "c5": (32, 8, 16384, 128, "v1", None),
        "b1h2l4k": (1, 2, 4096, 128, "v2", None), "b1h2l4k_unsplit": (1, 2, 4096, 128, "v2", 16),
+       "b2h2l16k": (2, 2, 16384, 128, "v2", 4),
        "d384": (32, 8, 1024, 384, "td", None), "d512": (32, 8, 1024, 512, "td", None)}
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
