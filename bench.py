@@ -343,6 +343,13 @@ EXTRA_SHAPES = (
     ("b1h2_l4k_unsplit", 1, 2, 4096, 128, "v2", 4, "all"),
 )
 SPLIT_PAIRS = ("b1h1_l16k", "b1h2_l4k")
+# each extra's entry in profiles/hbm_traffic.json (rocprofv3 PMC passes of scripts/run_kernel.py
+# at the same shape and plan; kernel-labelled there): L2 egress per launch beside the timing
+EXTRA_TRAFFIC = {"c2_fused": "c2", "d384_tiled_d": "d384", "d512_tiled_d": "d512", "c4_splitkv": "c4",
+                 "c4_splitkv_4_blocks_per_wg": "c4g4", "c4_splitkv_1_block_per_wg": "c4g1",
+                 "c4_splitkv_auto": "c4", "b1h1_l16k_splitkv": "b1h1l16k",
+                 "b1h1_l16k_unsplit": "b1h1l16k_unsplit", "b1h2_l4k_splitkv": "b1h2l4k",
+                 "b1h2_l4k_unsplit": "b1h2l4k_unsplit"}
 EXTRA_SETTLE_S = 0.1  # untimed back-to-back launches of each extra shape before its window
 
 
@@ -384,6 +391,9 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
         ms = ems / n
         rec.update(ms=round(ms, 4), tflops=round(f / (ms * 1e-3) / 1e12, 1),
                    frac=round(f / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4))
+        tr = extra_traffic(name, B, H, L, d)
+        if tr is not None:
+            rec["traffic"] = tr
         out[name] = rec
         del qq, kk, vv
     for base in SPLIT_PAIRS:  # split against unsplit, same shape
@@ -393,14 +403,29 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
     return out
 
 
-def load_traffic(config):
+def load_traffic(config, full=False):
+    """bytes per launch of profiles/hbm_traffic.json[config] (the whole record with full=True),
+    None when the table has no such entry."""
     path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     try:
         with open(path) as f:
             rec = json.load(f).get(config)
-        return None if rec is None else rec.get("bytes_per_launch")
+        return rec if full or rec is None else rec.get("bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def extra_traffic(name, B, H, L, d):
+    """the L2-egress record of an extra (measured in a PMC pass, not in this run) against its
+    algorithmic bytes (Q, K, V read once, O written once)."""
+    key = EXTRA_TRAFFIC.get(name)
+    rec = load_traffic(key, full=True) if key else None
+    if rec is None:
+        return None
+    alg = 4 * B * H * L * d * 2
+    return {"bytes_per_launch": int(rec["bytes_per_launch"]), "algorithmic_bytes": alg,
+            "ratio": round(rec["bytes_per_launch"] / alg, 2), "kernel": rec.get("kernel"),
+            "source": f"profiles/hbm_traffic.json[{key}] ({rec.get('source', 'PMC')})"}
 
 
 def sample_heads(B, H, n=16):

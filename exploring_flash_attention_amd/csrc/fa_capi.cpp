@@ -359,6 +359,10 @@ int v2_workspace(int64_t B, int64_t H, int64_t L, int64_t d, const SplitPlan& sp
     if (B * H * nqt > (int64_t)0x7fffffff / ns)
         return fail(FA_ERR_UNSUPPORTED, "split-KV grid of %lld x %d workgroups exceeds 2^31-1 "
                     "(raise kv_tiles_per_block)", (long long)(B * H * nqt), ns);
+    // the in-kernel combine counts arrivals and completions in 16-bit halves of one counter
+    if (ns > 0xffff)
+        return fail(FA_ERR_UNSUPPORTED, "split-KV with %d partials per query tile exceeds 65535 "
+                    "(raise kv_tiles_per_block)", ns);
     // one partial workgroup per query tile: the FA-v1 kernel, no workspace needed
     *bytes = ns == 1 ? 256 : v2_layout(B * H, L, d, ns, pe).total;
     return FA_OK;
@@ -563,6 +567,13 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     a.lse = (float*)((char*)workspace + w.lse_off);
     a.esc = (float*)((char*)workspace + w.esc_off);
     a.tile_group = tile_group((int64_t)a.nqt * ns * BH, ns, a.nqt);
+    // Hand-off order of fa_fwd16_kernel's combine (fa_fwd16_kernel.hpp): arrival first -- the
+    // last arriver's partial never stored, 1/S of the partial bytes saved twice -- costs a
+    // memory round trip on the tile's critical path when its workgroups finish together, so
+    // only for key blocks of >= 4096 keys.  Round 5, d = 128 bf16 (profiles/r05/ab,
+    // profiles/r05/hbm_traffic_r05.json): B1 H1 L16384 (4 blocks of 4096) 127.5 -> 127.2 us and
+    // 72.7 -> 64.1 MB per launch; B1 H2 L4096 (4 of 1024) 28.7 -> 31.0 us.
+    a.arrive_first = a.kv_per_split >= 4096;
     a.counters = (unsigned*)((char*)workspace + w.cnt_off);
     a.o_final = o;
     // the kernel leaves every counter at zero; clearing them here makes a call that follows

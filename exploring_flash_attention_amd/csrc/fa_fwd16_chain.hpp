@@ -325,9 +325,18 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     };
     // fused: the tile's partials summed in split order 0, 1, ... (fa_fwd16_kernel.hpp's combine,
     // the same order and arithmetic: bitwise the one-shot kernel's O) and O written
+    // The last block's partial is never stored: it is still in the registers (o, einv, elsev,
+    // eesc), rounded here exactly as part_store would round it; its ranges are empty (loads
+    // return 0 and move no bytes).
     auto combine = [&](int64_t grp, int64_t o_row0) {
         const int ns = a.nsplit;
+        const int own = ns - 1;
         auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
+        auto epi_c = [&](int sp) {
+            Epi ep = epi_of(blk_of(sp));
+            if (sp == own) ep = Epi{make_rsrc(a.lse, 0), make_rsrc(a.lse, 0), make_rsrc(a.lse, 0)};
+            return ep;
+        };
         const __amdgpu_buffer_rsrc_t ofin = make_rsrc(uni((const unsigned short*)a.o_final + o_row0), kBQ * ROWB);
         // (U key blocks' loads in flight at a time: the walk schedule runs this between tiles,
         // where nothing hides its latency; an index past the last block re-reads the last one,
@@ -341,9 +350,14 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 float lv[U], ev[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const Epi ep = epi_of(blk_of(sp0 + u < ns ? sp0 + u : ns - 1));
+                    const int sp = sp0 + u < ns ? sp0 + u : ns - 1;
+                    const Epi ep = epi_c(sp);
                     lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1));
                     ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
+                    if (sp == own) {
+                        lv[u] = elsev[QB];
+                        ev[u] = eesc[QB];
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -360,13 +374,23 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 u32x2 pv[U][NDB];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const Epi ep = epi_of(blk_of(sp0 + u < ns ? sp0 + u : ns - 1));
+                    const int sp = sp0 + u < ns ? sp0 + u : ns - 1;
+                    const Epi ep = epi_c(sp);
                     lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1));
                     ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
 #pragma unroll
                     for (int db = 0; db < NDB; ++db)
                         pv[u][db] = __builtin_bit_cast(
                             u32x2, __builtin_amdgcn_raw_buffer_load_b64(ep.o, frag_off(db * NQB + QB), 0, SC1));
+                    if (sp == own) {
+                        lv[u] = elsev[QB];
+                        ev[u] = eesc[QB];
+#pragma unroll
+                        for (int db = 0; db < NDB; ++db) {
+                            const f32x4 x = o[db][QB] * einv[QB];
+                            pv[u][db] = u32x2{pack2<_Float16>(x[0], x[1]), pack2<_Float16>(x[2], x[3])};
+                        }
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -631,9 +655,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 m[1] = mx[1];
                 if (!more) break;
             }
-            // the tile's last partial, then the combine (every wave's stores out first)
-            static_for<NF>([&](auto f_c) { part_store(f_c, prev_ep); });
-            lse_store(prev_ep);
+            // the combine, the last block's partial from the registers (the others' stores out
+            // first)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             combine(t0.grp, t0.o_row0);

@@ -497,62 +497,109 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             }
         }
     } else {
-        // Split-KV partials combined on chip (fa_fwd_kernel.hpp's protocol and workspace
-        // layout): every workgroup stores its normalised partial O (PT) and lse in FRAGMENT
-        // order -- lane-linear pieces, coalesced for the stores and the combine's loads; the
-        // workgroup that arrives last at its query tile's counter (stores sc1, vmcnt(0), a
-        // barrier, one agent-scope atomic) reads the other splits' partials and writes O.
+        // Split-KV partials combined on chip (fa_fwd_kernel.hpp's workspace layout): every
+        // workgroup but the last one at its query tile stores its normalised partial O (PT) and
+        // lse in FRAGMENT order -- lane-linear pieces, coalesced for the stores and the
+        // combine's loads -- with sc1 and drains them (vmcnt(0), a barrier); the last one sums
+        // all partials, its own from the registers, rounded exactly as its store would round
+        // them.  Who is last: one agent-scope atomic per workgroup on the tile's counter, in
+        // one of two orders (FwdArgs::arrive_first, chosen by the launcher):
+        //  * stores first, then the ARRIVAL count (low 16 bits): the last arriver has stored its
+        //    partial too but never reads it back;
+        //  * arrive_first: the ARRIVAL count first; all but the last then store and count their
+        //    COMPLETION (high 16 bits), and the last waits for the others' completions -- they
+        //    arrived, so they are running and only their stores are outstanding: the wait cannot
+        //    deadlock -- and its partial never leaves the registers.  One more memory round trip
+        //    on the tile's critical path when its workgroups finish together, so the launcher
+        //    takes it only for long key blocks (fa_capi.cpp).
         constexpr int SC1 = 16;                // cache-policy bit: sc1
         constexpr int NF = NDB * NQB;          // fragments (4 values) per lane
         constexpr int BLK = kBQ * D;           // partial elements per (split, tile) block
         const int64_t grp = bh * a.nqt + qt;
         auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
-        auto o_rsrc = [&](int sp) { return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, (int64_t)BLK * sizeof(PT)); };
-        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
-        auto e_rsrc = [&](int sp) { return make_rsrc(a.esc + blk_of(sp) * kBQ, (int64_t)kBQ * 4); };
+        // (the own block's ranges are empty in the combine: its loads return 0 and move no bytes)
+        auto o_rsrc = [&](int sp) {
+            return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, sp == split ? 0 : (int64_t)BLK * sizeof(PT));
+        };
+        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, sp == split ? 0 : (int64_t)kBQ * 4); };
+        auto e_rsrc = [&](int sp) { return make_rsrc(a.esc + blk_of(sp) * kBQ, sp == split ? 0 : (int64_t)kBQ * 4); };
         auto frag_off = [&](int f) { return (((wid * NF + f) * 64 + lane) * 4) * (int)sizeof(PT); };
         auto lse_off = [&](int qb) { return (wid * 32 + 16 * qb + n16) * 4; };
-        {
-            const __amdgpu_buffer_rsrc_t ors = o_rsrc(split), lrs = l_rsrc(split);
+        int* const last_flag = (int*)smem;  // LDS is free: the KV loop ended with a barrier
+        const bool af = a.arrive_first != 0;
+        auto arrive = [&]() {
+            if (tid == 0) {
+                const unsigned old = __hip_atomic_fetch_add(a.counters + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *last_flag = (old & 0xffffu) + 1 == (unsigned)a.nsplit;
+            }
+            __syncthreads();
+            return __builtin_amdgcn_readfirstlane(*last_flag);
+        };
+        int last = af ? arrive() : 0;
+        // this block's partial as stored: 16-bit pairs (or fp32) per fragment, lse of the row
+        using Frag = std::conditional_t<sizeof(PT) == 4, f32x4, u32x2>;
+        Frag mine[NQB][NDB];
+        float lse_mine[NQB];
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) {
+                const f32x4 x = ov[qb][db] * inv[qb];
+                if constexpr (sizeof(PT) == 4)
+                    mine[qb][db] = x;
+                else
+                    mine[qb][db] = u32x2{pack2<PH>(x[0], x[1]), pack2<PH>(x[2], x[3])};
+            }
+            // the row's lse as lane group 0 stores it
+            const float lse = m[qb] + __builtin_amdgcn_logf(lsum[qb]);
+            lse_mine[qb] = __int_as_float(__builtin_amdgcn_ds_bpermute(n16 * 4, __float_as_int(lse)));
+        }
+        if (!last) {
+            const __amdgpu_buffer_rsrc_t ors = make_rsrc((const PT*)a.o + blk_of(split) * BLK, (int64_t)BLK * sizeof(PT));
+            const __amdgpu_buffer_rsrc_t lrs = make_rsrc(a.lse + blk_of(split) * kBQ, (int64_t)kBQ * 4);
+            const __amdgpu_buffer_rsrc_t ers = make_rsrc(a.esc + blk_of(split) * kBQ, (int64_t)kBQ * 4);
 #pragma unroll
             for (int qb = 0; qb < NQB; ++qb) {
 #pragma unroll
                 for (int db = 0; db < NDB; ++db) {
-                    const f32x4 x = ov[qb][db] * inv[qb];
                     if constexpr (sizeof(PT) == 4)
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), ors, frag_off(db * NQB + qb), 0, SC1);
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, mine[qb][db]), ors,
+                                                               frag_off(db * NQB + qb), 0, SC1);
                     else
-                        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2<PH>(x[0], x[1]), pack2<PH>(x[2], x[3])}, ors,
-                                                              frag_off(db * NQB + qb), 0, SC1);
+                        __builtin_amdgcn_raw_buffer_store_b64(mine[qb][db], ors, frag_off(db * NQB + qb), 0, SC1);
                 }
                 if (g == 0) {
-                    const float lse = m[qb] + __builtin_amdgcn_logf(lsum[qb]);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse), lrs, lse_off(qb), 0, SC1);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse_mine[qb]), lrs, lse_off(qb), 0, SC1);
                     if constexpr (SCALED)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(esc[qb]), e_rsrc(split), lse_off(qb), 0, SC1);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(esc[qb]), ers, lse_off(qb), 0, SC1);
                 }
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (af) {
+                if (tid == 0) __hip_atomic_fetch_add(a.counters + grp, 0x10000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            last = arrive();
+            if (!last) return;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int* const last_flag = (int*)smem;  // LDS is free: the KV loop ended with a barrier
         if (tid == 0) {
-            const unsigned old = __hip_atomic_fetch_add(a.counters + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old + 1 == (unsigned)a.nsplit;
-            if (last) a.counters[grp] = 0;  // leave the counter zero for the next launch
-            *last_flag = last;
+            if (af) {
+                const unsigned want = (unsigned)(a.nsplit - 1) << 16;
+                while ((__hip_atomic_load(a.counters + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffff0000u) != want)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            a.counters[grp] = 0;  // leave the counter zero for the next launch
         }
         __syncthreads();
-        if (!*last_flag) return;
 
-        // Sum in split order 0, 1, ... whatever workgroup came last (its own partial is read
-        // back too), so that O is bitwise repeatable.
+        // Sum in split order 0, 1, ... whatever workgroup came last, so that O is bitwise
+        // repeatable.
         const int ns = a.nsplit;
-        auto load_val = [&](int sp, int f) -> f32x4 {
+        auto widen = [&](const Frag& u) -> f32x4 {
             if constexpr (sizeof(PT) == 4) {
-                return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(o_rsrc(sp), frag_off(f), 0, SC1));
+                return u;
             } else {
-                const u32x2 u = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(o_rsrc(sp), frag_off(f), 0, SC1));
                 // (16-bit halves by shifts: hipcc miscompiles a bit_cast of u[1] to a 2 x bf16 vector
                 // into a second copy of u[0] and narrows the load to one dword)
                 f32x4 r;
@@ -563,6 +610,12 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                 }
                 return r;
             }
+        };
+        auto load_frag = [&](int sp, int f) -> Frag {
+            if constexpr (sizeof(PT) == 4)
+                return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(o_rsrc(sp), frag_off(f), 0, SC1));
+            else
+                return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(o_rsrc(sp), frag_off(f), 0, SC1));
         };
         // U key blocks' loads in flight at a time (one at a time, the combine is a chain of
         // memory latencies: the chained walk's C4 run went -10 % -> +9.5 % with this); an index
@@ -577,9 +630,14 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                 float lv[U], ev[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(clampsp(sp0 + u)), lse_off(qb), 0, SC1));
+                    const int sp = clampsp(sp0 + u);
+                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1));
                     if constexpr (SCALED)
-                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(clampsp(sp0 + u)), lse_off(qb), 0, SC1));
+                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
+                    if (sp == split) {
+                        lv[u] = lse_mine[qb];
+                        ev[u] = esc[qb];
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -593,7 +651,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             float wsum = 0.f;
             for (int sp0 = 0; sp0 < ns; sp0 += U) {
                 float lv[U], ev[U];
-                f32x4 pv[U][NDB];
+                Frag pv[U][NDB];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int sp = clampsp(sp0 + u);
@@ -601,7 +659,13 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                     if constexpr (SCALED)
                         ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
 #pragma unroll
-                    for (int db = 0; db < NDB; ++db) pv[u][db] = load_val(sp, db * NQB + qb);
+                    for (int db = 0; db < NDB; ++db) pv[u][db] = load_frag(sp, db * NQB + qb);
+                    if (sp == split) {
+                        lv[u] = lse_mine[qb];
+                        ev[u] = esc[qb];
+#pragma unroll
+                        for (int db = 0; db < NDB; ++db) pv[u][db] = mine[qb][db];
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -609,7 +673,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                     float wv = wgt;
                     if constexpr (SCALED) wv = __builtin_amdgcn_ldexpf(wgt, (int)(ev[u] - E));
 #pragma unroll
-                    for (int db = 0; db < NDB; ++db) acc[db] += wv * pv[u][db];
+                    for (int db = 0; db < NDB; ++db) acc[db] += wv * widen(pv[u][db]);
                     wsum += wgt;
                 }
             }

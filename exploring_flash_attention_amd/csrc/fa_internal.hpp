@@ -81,6 +81,9 @@ struct FwdArgs {
     // of one query tile run together: Q re-read from L2, partials combined while hot), between:
     // both, for a group of tiles
     int tile_group;
+    // fused split mode, fa_fwd16_kernel: arrival counted before the partial stores, so that the
+    // last arriver never stores its own (fa_fwd16_kernel.hpp); 0: stores first
+    int arrive_first;
 };
 
 // (query tile, split, b*h) of work item w (after xcd_remap)

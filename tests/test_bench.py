@@ -111,3 +111,16 @@ def test_kernel_labels_follow_the_dispatch():
     assert bench.fwd_kernel_name(128, 1024, "final", items=256, cus=256).startswith("fa_fwd16_kernel")
     assert bench.fwd_kernel_name(128, 1000, "final").startswith("fa_fwd_kernel")
     assert bench.fwd_kernel_name(32, 1024, "final").startswith("fa_fwd_kernel")
+
+
+def test_extra_traffic_records_are_labelled():
+    """Every bench extra with a traffic entry reports measured bytes, the algorithmic bytes and
+    the kernel the PMC pass measured."""
+    import bench
+    for name, B, H, L, d, *_ in bench.EXTRA_SHAPES:
+        tr = bench.extra_traffic(name, B, H, L, d)
+        if tr is None:
+            continue
+        assert tr["algorithmic_bytes"] == 8 * B * H * L * d
+        assert tr["bytes_per_launch"] > 0 and tr["ratio"] > 0
+        assert tr["kernel"] and tr["kernel"] != "(unlabelled)", name
