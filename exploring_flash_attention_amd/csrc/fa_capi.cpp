@@ -120,8 +120,8 @@ int hip_fail(hipError_t e, const char* what) {
 
 // query rows per workgroup and keys per KV tile of the kernel serving dtype e (and head dim d)
 int rows_per_block(fa::Elem e, int64_t d = 128) {
-    if (wide_d(d)) return fa::dtiled_rows_per_block();
-    return e == fa::Elem::F64 ? fa::fwd64_rows_per_block() : fa::kBQ;
+    if (e == fa::Elem::F64) return fa::fwd64_rows_per_block();  // (its d-tiled kernel's too)
+    return wide_d(d) ? fa::dtiled_rows_per_block() : fa::kBQ;
 }
 int keys_per_tile(fa::Elem e, int64_t d) {
     if (e == fa::Elem::F64) return fa::fwd64_keys_per_tile();
@@ -188,9 +188,9 @@ int apply_scale(fa::FwdArgs& a, double softmax_scale) {
 }
 
 // d = 384 / 512: the d-tiled kernels with the given (requested) d tiles; their query tile is
-// 64 rows (dtiled_rows_per_block; the fp64 kernel's too)
+// rows_per_block(e, d) rows (dtiled_rows_per_block; the fp64 kernel's 64)
 hipError_t launch_wide(fa::Elem e, int d, fa::FwdArgs a, int d_tile_qk, int d_tile_v, hipStream_t s) {
-    a.nqt = (int)((a.Lq + fa::dtiled_rows_per_block() - 1) / fa::dtiled_rows_per_block());
+    a.nqt = (int)((a.Lq + rows_per_block(e, d) - 1) / rows_per_block(e, d));
     a.d_tile_qk = dtile_eff(d_tile_qk);
     a.d_tile_v = dtile_eff(d_tile_v);
     return e == fa::Elem::F64 ? fa::launch_fwd64_dtiled(d, a, s) : fa::launch_fwd_dtiled(e, d, a, s);
@@ -383,7 +383,7 @@ int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int
         return fail(FA_ERR_UNSUPPORTED, "head dim d=%lld has no kernel", (long long)d);
     if (wide_d(d)) {  // the d-tiled kernels: 64 query rows, K / V chunks of at most 128 columns
         if (e == fa::Elem::F64) {
-            if (bq) *bq = fa::dtiled_rows_per_block();
+            if (bq) *bq = fa::fwd64_rows_per_block();
             if (threads) *threads = fa::kThreads;
             if (lds_bytes) *lds_bytes = (64 + 2 * 16) * 129 * 8 + 4 * 16 * 17 * 8;
         } else {
