@@ -343,35 +343,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         // harmless to the maxima and given weight 0 in the sums -- the same sums in the same
         // order, as acc never holds -0)
         constexpr int U = 4;
+        // (at most U blocks: everything loaded in one batch, one memory round trip, not two)
         static_for<NQB>([&](auto qb_c) {
             constexpr int QB = decltype(qb_c)::value;
-            float Mx = -INFINITY, E = -1000.f;
-            for (int sp0 = 0; sp0 < ns; sp0 += U) {
-                float lv[U], ev[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sp = sp0 + u < ns ? sp0 + u : ns - 1;
-                    const Epi ep = epi_c(sp);
-                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1));
-                    ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
-                    if (sp == own) {
-                        lv[u] = elsev[QB];
-                        ev[u] = eesc[QB];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    Mx = fmaxf(Mx, lv[u]);
-                    E = fmaxf(E, ev[u]);
-                }
-            }
-            f32x4 acc[NDB];
-#pragma unroll
-            for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
-            float wsum = 0.f;
-            for (int sp0 = 0; sp0 < ns; sp0 += U) {
-                float lv[U], ev[U];
-                u32x2 pv[U][NDB];
+            auto load_batch = [&](int sp0, float (&lv)[U], float (&ev)[U], u32x2 (&pv)[U][NDB]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int sp = sp0 + u < ns ? sp0 + u : ns - 1;
@@ -392,6 +367,13 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                         }
                     }
                 }
+            };
+            float Mx = -INFINITY, E = -1000.f;
+            f32x4 acc[NDB];
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
+            float wsum = 0.f;
+            auto accumulate = [&](int sp0, const float (&lv)[U], const float (&ev)[U], const u32x2 (&pv)[U][NDB]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const float wgt = sp0 + u < ns ? __builtin_amdgcn_exp2f(lv[u] - Mx) : 0.f;
@@ -407,6 +389,43 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                         acc[db] += wv * r;
                     }
                     wsum += wgt;
+                }
+            };
+            if (ns <= U) {
+                float lv[U], ev[U];
+                u32x2 pv[U][NDB];
+                load_batch(0, lv, ev, pv);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    Mx = fmaxf(Mx, lv[u]);
+                    E = fmaxf(E, ev[u]);
+                }
+                accumulate(0, lv, ev, pv);
+            } else {
+                for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                    float lv[U], ev[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int sp = sp0 + u < ns ? sp0 + u : ns - 1;
+                        const Epi ep = epi_c(sp);
+                        lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.l, lse_off(QB), 0, SC1));
+                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ep.e, lse_off(QB), 0, SC1));
+                        if (sp == own) {
+                            lv[u] = elsev[QB];
+                            ev[u] = eesc[QB];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        Mx = fmaxf(Mx, lv[u]);
+                        E = fmaxf(E, ev[u]);
+                    }
+                }
+                for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                    float lv[U], ev[U];
+                    u32x2 pv[U][NDB];
+                    load_batch(sp0, lv, ev, pv);
+                    accumulate(sp0, lv, ev, pv);
                 }
             }
             const float inv_w = 1.f / wsum;
@@ -564,11 +583,14 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // prologue of an item's first tile (fa_fwd16_kernel.hpp's): Q, K(0), V(0), K(1); S(0)
     f32x4 sa[NKB][NQB], sb[NKB][NQB];
     float mx[NQB];
-    auto prologue = [&](const Item& it) {
+    // (in two halves: the walk issues a tile's loads before the previous tile's combine)
+    auto prologue_issue = [&](const Item& it) {
         load_q(it);
         dma_tile(it.k, kring, 0);
         dma_tile(it.v, vring, 0);
         dma_tile(it.k, kring + TILEB, 1);
+    };
+    auto prologue_finish = [&]() {
 #pragma unroll
         for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
@@ -579,6 +601,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         m[0] = mx[0];  // the reference max starts at tile 0's row max (no step-0 rescale)
         m[1] = mx[1];
         __syncthreads();
+    };
+    auto prologue = [&](const Item& it) {
+        prologue_issue(it);
+        prologue_finish();
     };
 
     using C0 = std::integral_constant<int, 0>;
@@ -630,7 +656,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         const int ns = a.nsplit;
         for (int j = 0; j < nmine; ++j) {
             const Item t0 = j == 0 ? cur : item(j);
-            prologue(t0);
+            if (j == 0) prologue_issue(t0);
+            prologue_finish();
             Epi prev_ep = enone;
             for (int sp = 0;; ++sp) {
                 const bool more = sp + 1 < ns;
@@ -656,10 +683,23 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 if (!more) break;
             }
             // the combine, the last block's partial from the registers (the others' stores out
-            // first)
+            // first), with the next tile's Q and first K / V tiles already on their way (the
+            // ring is free: the last step's barrier retired its reads)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            // (the K / V tiles only before the combine -- Q^T after it, so that its registers
+            // stay free for the combine: the whole prologue before it spilled; A/B in
+            // profiles/r05/ab/r05t_*, ov2 = this, ov0 = after the combine: B1 H2 L4096 29.1 ->
+            // 28.2 us, C4 at 4 partials +0.4 %, both with the one-batch combine)
+            const bool nx = j + 1 < nmine;
+            const Item tn = item(nx ? j + 1 : j);
+            if (nx) {
+                dma_tile(tn.k, kring, 0);
+                dma_tile(tn.v, vring, 0);
+                dma_tile(tn.k, kring + TILEB, 1);
+            }
             combine(t0.grp, t0.o_row0);
+            if (nx) load_q(tn);
         }
     }
 }

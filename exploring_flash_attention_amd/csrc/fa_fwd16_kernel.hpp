@@ -623,35 +623,11 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
         // the sums -- the same sums in the same order (acc never holds -0)
         constexpr int U = sizeof(PT) == 4 ? 2 : 4;
         auto clampsp = [&](int sp) { return sp < ns ? sp : ns - 1; };
+        // (at most U blocks -- the library's splits at d = 128 -- everything is loaded in one
+        // batch: one memory round trip on the tile's critical path instead of two)
 #pragma unroll
         for (int qb = 0; qb < NQB; ++qb) {
-            float Mx = -INFINITY, E = -1000.f;
-            for (int sp0 = 0; sp0 < ns; sp0 += U) {
-                float lv[U], ev[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sp = clampsp(sp0 + u);
-                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1));
-                    if constexpr (SCALED)
-                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
-                    if (sp == split) {
-                        lv[u] = lse_mine[qb];
-                        ev[u] = esc[qb];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    Mx = fmaxf(Mx, lv[u]);
-                    if constexpr (SCALED) E = fmaxf(E, ev[u]);
-                }
-            }
-            f32x4 acc[NDB];
-#pragma unroll
-            for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
-            float wsum = 0.f;
-            for (int sp0 = 0; sp0 < ns; sp0 += U) {
-                float lv[U], ev[U];
-                Frag pv[U][NDB];
+            auto load_batch = [&](int sp0, float (&lv)[U], float (&ev)[U], Frag (&pv)[U][NDB]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int sp = clampsp(sp0 + u);
@@ -667,6 +643,13 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                         for (int db = 0; db < NDB; ++db) pv[u][db] = mine[qb][db];
                     }
                 }
+            };
+            float Mx = -INFINITY, E = -1000.f;
+            f32x4 acc[NDB];
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) acc[db] = f32x4{};
+            float wsum = 0.f;
+            auto accumulate = [&](int sp0, const float (&lv)[U], const float (&ev)[U], const Frag (&pv)[U][NDB]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const float wgt = sp0 + u < ns ? __builtin_amdgcn_exp2f(lv[u] - Mx) : 0.f;
@@ -675,6 +658,43 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
 #pragma unroll
                     for (int db = 0; db < NDB; ++db) acc[db] += wv * widen(pv[u][db]);
                     wsum += wgt;
+                }
+            };
+            if (ns <= U) {
+                float lv[U], ev[U];
+                Frag pv[U][NDB];
+                load_batch(0, lv, ev, pv);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    Mx = fmaxf(Mx, lv[u]);
+                    if constexpr (SCALED) E = fmaxf(E, ev[u]);
+                }
+                accumulate(0, lv, ev, pv);
+            } else {
+                for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                    float lv[U], ev[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int sp = clampsp(sp0 + u);
+                        lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1));
+                        if constexpr (SCALED)
+                            ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
+                        if (sp == split) {
+                            lv[u] = lse_mine[qb];
+                            ev[u] = esc[qb];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        Mx = fmaxf(Mx, lv[u]);
+                        if constexpr (SCALED) E = fmaxf(E, ev[u]);
+                    }
+                }
+                for (int sp0 = 0; sp0 < ns; sp0 += U) {
+                    float lv[U], ev[U];
+                    Frag pv[U][NDB];
+                    load_batch(sp0, lv, ev, pv);
+                    accumulate(sp0, lv, ev, pv);
                 }
             }
             float inv_w = 1.f / wsum;
