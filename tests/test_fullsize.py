@@ -238,3 +238,32 @@ def test_chain_kernel_shapes(gpu, B, H, L):
     pick = lambda t: t.reshape(B * H, L, d)[idx][None].cpu()
     ref = attention_fp64(pick(q).double().numpy(), pick(k).double().numpy(), pick(v).double().numpy())
     _gate(pick(o1), ref, torch.bfloat16)
+
+
+@pytest.mark.parametrize("shape,kvt,group,partials", [
+    ((1, 1, 16384), 4, None, 4),        # one-shot grid, 4 blocks of 4096 keys: arrival-first hand-off
+    ((1, 2, 4096), 4, None, 4),         # one-shot grid, store-first hand-off, one-batch combine
+    ((2, 2, 16384), 4, 4, 16),          # the chained walk (512 tiles), 16 partials: two-pass combine
+    ((1, 8, 16384), 4, 16, 4),          # the walk at 4 partials of 4096 keys: one-batch combine
+], ids=["b1h1-l16k", "b1h2-l4k", "b2h2-l16k-walk16", "b1h8-l16k-walk4"])
+def test_long_sequence_split_paths(gpu, shape, kvt, group, partials):
+    """The split-KV schedules of the low-parallelism shapes (the bench extras and the chained
+    walk) against the fp64 oracle on 512 sampled query rows of every head -- first and last
+    rows, every query tile -- with the full key range; bitwise repeatable across two launches
+    on a reused workspace (the counters left at zero)."""
+    from exploring_flash_attention_amd import ops
+    b, h, L = shape
+    g = torch.Generator(device="cuda").manual_seed(L + h)
+    q, k, v = (torch.randn(b, h, L, 128, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    _, _, parts = ops.v2_split_plan(b, h, L, 128, kvt, q.dtype, blocks_per_workgroup=group)
+    assert parts == partials, parts
+    nbytes, _ = ops.v2_workspace_bytes(b, h, L, 128, kvt, blocks_per_workgroup=group)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
+    o1 = ops.attention_v2(q, k, v, kvt, workspace=ws, blocks_per_workgroup=group)
+    o2 = ops.attention_v2(q, k, v, kvt, workspace=ws, blocks_per_workgroup=group)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    rows = torch.tensor(sorted({round(i * (L - 1) / 511) for i in range(512)}), device=gpu)
+    qs = q[:, :, rows].cpu().double().numpy()
+    ref = attention_fp64(qs, k.cpu().double().numpy(), v.cpu().double().numpy())
+    _gate(o1[:, :, rows].cpu(), ref, torch.bfloat16, label=f"long split B{b} H{h} L{L} ({partials} partials)")
