@@ -61,7 +61,7 @@ def pytest_terminal_summary(terminalreporter):
     tot = sum(r["count"] for r in recs)
     of = sum(r["of"] for r in recs)
     for r in recs:
-        if r["count"] or r["label"].startswith("fullsize"):
+        if r["count"] or r["label"].startswith(("fullsize", "long split")):
             tr.write_line(f"{r['label']}: {r['count']} of {r['of']}"
                           + (f" (max |ref| {r['max_abs_ref']:.2e}, max |err| {r['max_err']:.2e}, "
                              f"max rel {r['max_rel']:.2f})" if r["count"] else ""))
