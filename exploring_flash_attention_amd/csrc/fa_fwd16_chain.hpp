@@ -39,6 +39,12 @@
 #pragma once
 #include "fa_fwd16_kernel.hpp"
 
+// schedule switch kept for A/B builds (scripts/build_lite.sh); the default is the measured
+// choice
+#ifndef FA_EPI_LATE
+#define FA_EPI_LATE 1  // EPI step: DMA pieces first, the previous item's stores behind them
+#endif
+
 namespace fa {
 
 // MODE kFinal: items are query tiles, O stored.  MODE kFused (split-KV, scaled fp16 partials in
@@ -515,11 +521,25 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             constexpr int E0 = S * EXPA / 16, E1 = (S + 1) * EXPA / 16;
             static_for<E1 - E0>([&](auto j_c) { ex(std::integral_constant<int, E0 + decltype(j_c)::value>{}); });
             if constexpr (S >= 6 && S < 14) cvt(std::integral_constant<int, S - 6>{});  // key step 0 packs
-            if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
-            if constexpr (EPI && !FUSED && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ep.o);
-            if constexpr (EPI && FUSED) {
-                part_store(std::integral_constant<int, S>{}, ep);
-                if constexpr (S == 0) lse_store(ep);
+            if constexpr (EPI && FA_EPI_LATE) {
+                // the DMA pieces in slots 0..7, the previous item's stores behind them in 8..15,
+                // so that the closing barrier waits for the pieces only (vmcnt counts stores too,
+                // in issue order; __syncthreads' fence would drain the stores: their write
+                // latency, 1-2 us, at every item boundary)
+                if constexpr (S < 8) dma(std::integral_constant<int, S>{});
+                if constexpr (!FUSED && S >= 8) store_group(std::integral_constant<int, S - 8>{}, ep.o);
+                if constexpr (FUSED && S >= 8) {
+                    part_store(std::integral_constant<int, 2 * (S - 8)>{}, ep);
+                    part_store(std::integral_constant<int, 2 * (S - 8) + 1>{}, ep);
+                    if constexpr (S == 8) lse_store(ep);
+                }
+            } else {
+                if constexpr (S % 2 == 1) dma(std::integral_constant<int, S / 2>{});
+                if constexpr (EPI && !FUSED && S % 2 == 0) store_group(std::integral_constant<int, S / 2>{}, ep.o);
+                if constexpr (EPI && FUSED) {
+                    part_store(std::integral_constant<int, S>{}, ep);
+                    if constexpr (S == 0) lse_store(ep);
+                }
             }
             if constexpr (MORE) fence();
         });
@@ -575,6 +595,10 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             // first QK^T MFMA the compiler makes wait for them
             static_assert(NQB * NKS == 8, "vmcnt count of the Q loads");
             asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        } else if constexpr (EPI && FA_EPI_LATE) {
+            // every DMA piece landed; the stores (the youngest NST operations) stay in flight
+            constexpr int NST = FUSED ? NF + 2 * NQB : 8;
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
         } else {
             __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed
         }
