@@ -453,10 +453,24 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // still in the registers: phase A stores it -- final: one 16-byte row store per even slot,
     // fused: one partial fragment per slot and the {lse, e} pairs -- and phase B's first P.V /
     // row-sum MFMAs start from zero instead of accumulating).
+#if FA_STAMPS
+    int stampv = 0, stamp_k = 0;
+    const unsigned long long stamp_rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     auto step = [&](auto par_c, auto flags_c, f32x4 (&sc)[NKB][NQB], f32x4 (&sn)[NKB][NQB], float (&mx)[NQB],
                     __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs, const Item& nxt, const Epi& ep) {
         constexpr int P = decltype(par_c)::value;
         constexpr int F = decltype(flags_c)::value;
+#if FA_STAMPS
+        // (diagnostic builds: the start of each of the first 64 steps, lane k of a VGPR -- no
+        // memory operation inside the loop; written out after it)
+        if (stamp_k < 64)
+        {
+            const int tnow = (int)(unsigned)__builtin_amdgcn_s_memtime();
+            stampv = lane == stamp_k ? tnow : stampv;
+        }
+        ++stamp_k;
+#endif
         constexpr bool MORE = F & 1;
         constexpr bool DMAK = F & 4;
         constexpr bool QNEXT = F & 8;
@@ -670,6 +684,22 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             cur = nxt;
         }
         static_for<8>([&](auto g_c) { store_group(g_c, prev_ep.o); });
+#if FA_STAMPS
+        // slots per workgroup (80): 0..63 step starts (s_memtime, low 32 bits), 64 loop end,
+        // 65 / 66 s_memrealtime at entry / loop end, 67 HW_ID, 68 XCC_ID (scripts/chain_stamps.py)
+        {
+            const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+            const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+            if (tid < 64) g_fa_stamps[blockIdx.x * 80 + tid] = (unsigned)stampv;
+            if (tid == 0) {
+                g_fa_stamps[blockIdx.x * 80 + 64] = (unsigned)t_end;
+                g_fa_stamps[blockIdx.x * 80 + 65] = stamp_rt0;
+                g_fa_stamps[blockIdx.x * 80 + 66] = rt_end;
+                g_fa_stamps[blockIdx.x * 80 + 67] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+                g_fa_stamps[blockIdx.x * 80 + 68] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+            }
+        }
+#endif
     } else {
         // Split-KV, the reference's layout (one partial per key block in the workspace,
         // flash_attention_v2/CUDA/flash_attention_v2.h:243-341): a workgroup walks the key blocks
