@@ -161,7 +161,10 @@ int fa_fwd_v1_tiled_d_scaled(const void* q, const void* k, const void* v, void* 
  * block) is kv_tiles_per_block * bk keys (bk from fa_kernel_geometry).  partial_dtype is
  * FA_DTYPE_FP32, the input dtype or FA_DTYPE_FP16_SCALED.  *num_splits (may be NULL)
  * receives the number of key blocks.  The size covers the partials fa_fwd_v2 actually moves
- * through the workspace (fa_fwd_v2_split_plan); it depends on the device's occupancy. */
+ * through the workspace (fa_fwd_v2_split_plan); it depends on the device's occupancy.
+ * FA_ERR_UNSUPPORTED when the grid of (query tile, partial, b*h) workgroups exceeds 2^31 - 1
+ * or a query tile would have more than 65535 partials (the in-kernel combine counts arrivals
+ * and completions in 16-bit halves of one counter): raise kv_tiles_per_block. */
 int fa_fwd_v2_workspace_size(int64_t B, int64_t H, int64_t L, int64_t d,
                              int kv_tiles_per_block, int dtype, int partial_dtype,
                              size_t* bytes, int* num_splits);
