@@ -1,7 +1,7 @@
-# round 5, call n: GPU suite, smoke, default bench on the walk build
+# round 5, calls n / final: GPU suite, smoke, default bench
 set -u
 cd "${GRAFT_REPO_ROOT}"
-O=gpurun_out/r05n
+O=gpurun_out/r05final
 mkdir -p $O
 export PYTHONPATH=$PWD
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
