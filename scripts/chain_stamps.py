@@ -76,6 +76,19 @@ def main():
     end_us = (rt1 - rt0.min()) / 100.0
     print(f"  entry spread {start_us.max():.2f} us, loop end min {end_us.min():.2f} median "
           f"{np.median(end_us):.2f} max {end_us.max():.2f} us")
+    # the two workgroups of a CU (HW_ID bits 8..15: CU, SH, SE; plus the XCC): end-time gap
+    hw = st[:, 67].astype(np.int64)
+    cu_key = (st[:, 68].astype(np.int64) & 0xF) * 256 + ((hw >> 8) & 0xFF)
+    gaps, first_faster = [], 0
+    for key in set(cu_key.tolist()):
+        idx = np.nonzero(cu_key == key)[0]
+        if len(idx) == 2:
+            a, b = sorted(idx, key=lambda i: rt0[i])
+            gaps.append(abs(end_us[a] - end_us[b]))
+            first_faster += end_us[a] < end_us[b]
+    if gaps:
+        print(f"  CU pairs {len(gaps)}: end gap median {np.median(gaps):.2f} p90 {np.percentile(gaps, 90):.2f} us; "
+              f"the earlier-started one ends first in {first_faster} of {len(gaps)}")
     xcc = st[:, 68].astype(np.int64) & 0xF
     for x in sorted(set(xcc.tolist())):
         sel = xcc == x
