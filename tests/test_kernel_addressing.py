@@ -216,6 +216,51 @@ def test_fused_split_in_bounds(B, H, L, group, order):
            tile_group={"qtile-fastest": 0, "split-fastest": 1, "tile-group-4": 4}[order])
 
 
+@pytest.mark.parametrize("cus", [256, 80])
+@pytest.mark.parametrize("B,H,L,group", [(32, 8, 4096, 1), (32, 8, 4096, 4), (2, 2, 16384, 4), (1, 8, 16384, 16),
+                                         (3, 5, 2048, 2)],
+                         ids=["C4-16-partials", "C4-4-partials", "b2h2-l16k", "b1h8-l16k", "odd-heads"])
+def test_chain_walk_in_bounds(B, H, L, group, cus):
+    """The fused chain (fa_fwd16_chain.hpp, MODE kFused -- the walk): under fa_fwd.hip's
+    conditions (keys per block a multiple of 128 and >= 256, whole query tiles, at least one
+    query tile per workgroup of the 2-per-CU grid) every query tile is walked by exactly one
+    workgroup, over key blocks 0..ns-1; every K / V tile of every block, every partial block
+    (all but the last, stored; every one, read by the combine) and every O row lies inside its
+    buffer."""
+    d, kvt = 128, 4
+    kb, per, ppt, nbytes = _plan(B, H, L, d, kvt, group)
+    BH, nqt = B * H, L // KBQ
+    tiles, grid = BH * nqt, 2 * cus // 8 * 8
+    kvps = min(kvt * 64 * per, L)
+    if not (ppt > 1 and kvps % 128 == 0 and kvps >= 256 and L % kvps == 0 and L % KBQ == 0 and tiles >= grid):
+        pytest.skip("the launcher runs the one-shot kernel for this shape")
+    assert ppt * kvps == L
+    lists = chain_items(tiles, grid)
+    flat = np.array([w for lst in lists for w in lst], dtype=np.int64)
+    assert sorted(flat.tolist()) == list(range(tiles)) and all(len(lst) > 0 for lst in lists)
+    rows = ppt * BH * nqt * KBQ
+    o_bytes = a256(rows * d * 2)
+    ws_o = Alloc("ws partials", o_bytes)
+    ws_lse = Alloc("ws lse", a256(rows * 4))
+    q, k, v, o = (_tensor(n, B, H, L, d) for n in "qkvo")
+    qt, bh = flat % nqt, flat // nqt
+    grp = bh * nqt + qt
+    q.check(2 * (bh * L + qt * KBQ) * d, KBQ * 256, "walk Q tile")
+    o.check(2 * (bh * L + qt * KBQ) * d, KBQ * 256, "walk O tile (combine)")
+    BLK, TILEB = KBQ * d, 64 * 256
+    for sp in range(ppt):
+        kv0 = 2 * (bh * L + sp * kvps) * d
+        for t in range(kvps // 64):
+            k.check(kv0 + t * TILEB, TILEB, "walk K tile")
+            v.check(kv0 + t * TILEB, TILEB, "walk V tile")
+        blk = sp * BH * nqt + grp
+        ws_o.check(blk * BLK * 2, BLK * 2, "walk partial block")
+        ws_lse.check(blk * KBQ * 4, KBQ * 4, "walk lse / e block")
+    # every block of every tile is written by exactly one workgroup (the tile's walker)
+    blks = (np.arange(ppt)[:, None] * BH * nqt + grp[None, :]).ravel()
+    assert len(np.unique(blks)) == ppt * tiles
+
+
 @pytest.mark.parametrize("W", [2, 8])
 @pytest.mark.parametrize("L", [16384, 2048])
 def test_multi_gpu_partials_in_bounds(W, L):
