@@ -737,14 +737,13 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
                 if (!more) break;
             }
             // the combine, the last block's partial from the registers (the others' stores out
-            // first), with the next tile's Q and first K / V tiles already on their way (the
-            // ring is free: the last step's barrier retired its reads)
+            // first), with the next tile's first K / V tiles already on their way (the ring is
+            // free: the last step's barrier retired its reads) and its Q^T loaded after it, so
+            // that those registers stay free for the combine (the whole prologue before it
+            // spilled).  A/B (profiles/r05/ab/r05t_*, ov2 = this, ov0 = all after the combine):
+            // C4 at 4 partials +0.2 %, at 16 within noise.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            // (the K / V tiles only before the combine -- Q^T after it, so that its registers
-            // stay free for the combine: the whole prologue before it spilled; A/B in
-            // profiles/r05/ab/r05t_*, ov2 = this, ov0 = after the combine: B1 H2 L4096 29.1 ->
-            // 28.2 us, C4 at 4 partials +0.4 %, both with the one-batch combine)
             const bool nx = j + 1 < nmine;
             const Item tn = item(nx ? j + 1 : j);
             if (nx) {
