@@ -245,7 +245,8 @@ def test_chain_kernel_shapes(gpu, B, H, L):
     ((1, 2, 4096), 4, None, 4),         # one-shot grid, store-first hand-off, one-batch combine
     ((2, 2, 16384), 4, 4, 16),          # the chained walk (512 tiles), 16 partials: two-pass combine
     ((1, 8, 16384), 4, 16, 4),          # the walk at 4 partials of 4096 keys: one-batch combine
-], ids=["b1h1-l16k", "b1h2-l4k", "b2h2-l16k-walk16", "b1h8-l16k-walk4"])
+    ((1, 3, 16384), 4, None, 2),        # one-shot, arrival first, 768 workgroups: some queued
+], ids=["b1h1-l16k", "b1h2-l4k", "b2h2-l16k-walk16", "b1h8-l16k-walk4", "b1h3-l16k-queued"])
 def test_long_sequence_split_paths(gpu, shape, kvt, group, partials):
     """The split-KV schedules of the low-parallelism shapes (the bench extras and the chained
     walk) against the fp64 oracle on 512 sampled query rows of every head -- first and last
