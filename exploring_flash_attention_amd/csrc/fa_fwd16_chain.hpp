@@ -453,10 +453,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     // still in the registers: phase A stores it -- final: one 16-byte row store per even slot,
     // fused: one partial fragment per slot and the {lse, e} pairs -- and phase B's first P.V /
     // row-sum MFMAs start from zero instead of accumulating).
-#ifndef FA_PRIOBAL
-#define FA_PRIOBAL 0  // A/B: the CU's two workgroups take turns at the higher issue priority per item
-#endif
-    int prio_boost = 0;
 #if FA_STAMPS
     int stampv = 0, stamp_k = 0;
     const unsigned long long stamp_rt0 = __builtin_amdgcn_s_memrealtime();
@@ -517,16 +513,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         };
 
         // ---- phase A: QK^T(t+1) || exponentials of t (and, EPI, the previous item's O stores)
-#if FA_PRIOBAL
-        if constexpr (MORE) {
-            if (prio_boost)
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(1);
-        }
-#else
         if constexpr (MORE) __builtin_amdgcn_s_setprio(1);
-#endif
         u32x4 kf[KA + 1];
         if constexpr (MORE) {
 #pragma unroll
@@ -572,14 +559,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         });
 
         // ---- phase B: P.V(t) || exponentials of t (rest), row max of t+1
-#if FA_PRIOBAL
-        if (prio_boost)
-            __builtin_amdgcn_s_setprio(1);
-        else
-            __builtin_amdgcn_s_setprio(0);
-#else
         __builtin_amdgcn_s_setprio(0);
-#endif
         if constexpr (QNEXT) {  // phase A read the current Q^T for the last time
             load_q(nxt);
             fence();
@@ -678,7 +658,6 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         for (int j = 0;; ++j) {
             const bool more = j + 1 < nmine;
             const Item nxt = item(more ? j + 1 : j);
-            prio_boost = __builtin_amdgcn_readfirstlane(((int)(blockIdx.x >= gridDim.x / 2) + j) & 1);
             // t = 0, 1 (step 0 stores the previous item's O)
             step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
                  nxt, prev_ep);
