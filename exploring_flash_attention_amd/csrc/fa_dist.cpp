@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../../include/fa_mi355x_dist.h"
-#include "fa_dist_schedule.hpp"
+#include "fa_dist_ops.hpp"
 
 static_assert(sizeof(ncclUniqueId) == FA_DIST_UNIQUE_ID_BYTES, "ncclUniqueId size");
 
@@ -58,81 +58,47 @@ void destroy(Comm* c) {
     delete c;
 }
 
-size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+using fa::dist::esize;
+using fa::dist::Layout;
+using fa::dist::layout;
+using fa::dist::lsize;
 
-size_t esize(int dtype) { return dtype == FA_DTYPE_FP64 ? 8 : dtype == FA_DTYPE_FP32 ? 4 : 2; }
-// lse bytes per row: fp64 for fp64 inputs; {lse, e} for scaled fp16 partials
-size_t lsize(int dtype, int pdtype) {
-    return dtype == FA_DTYPE_FP64 ? 8 : pdtype == FA_DTYPE_FP16_SCALED ? 8 : 4;
-}
-
-struct Layout {
-    size_t part_bytes, lse_bytes;  // one side (send or receive)
-    size_t send_o, send_lse, recv_o, recv_lse, gather, total;
-};
-
-Layout layout(int64_t BH, int64_t L, int64_t d, int dtype, int pdtype) {
-    Layout w{};
-    const size_t rows = (size_t)BH * L;  // W chunks of BH * L/W rows
-    w.part_bytes = align256(rows * d * esize(pdtype));
-    w.lse_bytes = align256(rows * lsize(dtype, pdtype));
-    w.send_o = 0;
-    w.send_lse = w.send_o + w.part_bytes;
-    w.recv_o = w.send_lse + w.lse_bytes;
-    w.recv_lse = w.recv_o + w.part_bytes;
-    w.gather = w.recv_lse + w.lse_bytes;
-    w.total = w.gather + align256(rows * d * esize(dtype));
-    return w;
-}
-
-
-// The HIP / RCCL operations of fa_dist_schedule.hpp's run_exchange for one call.
-struct RcclOps {
-    Comm* c;
-    char* ws;
-    const void *q, *k, *v;
-    int64_t B, H, L, Lc, d;
-    int dtype, pdtype;
-    hipStream_t s;
-    int partial_chunk(int p, size_t o_off, size_t l_off) {
-        // a q row-range view in place: rows [p*Lc, (p+1)*Lc) of every head
-        const int64_t qst[3] = {H * L * d, L * d, d};
-        const char* qp = (const char*)q + (size_t)p * Lc * d * esize(dtype);
-        if (int st = fa_fwd_partial_ex(qp, k, v, ws + o_off, ws + l_off, B, H, Lc, Lc, d, Lc, qst, dtype, pdtype, s))
+// The HIP / RCCL primitives under fa_dist_ops.hpp's ExchangeOps (its Api): each maps the
+// library's error to a status code with the message in g_err.
+struct HipRcclApi {
+    using Stream = hipStream_t;
+    using Event = hipEvent_t;
+    ncclComm_t nccl;
+    int fwd_partial_ex(const void* q, const void* k, const void* v, void* o, void* lse, int64_t B, int64_t H,
+                       int64_t Lq, int64_t Lk, int64_t d, int64_t chunk_rows, const int64_t* qst, int dtype,
+                       int pdtype, Stream s) {
+        if (int st = fa_fwd_partial_ex(q, k, v, o, lse, B, H, Lq, Lk, d, chunk_rows, qst, dtype, pdtype, s))
             return core_fail(st, "fa_fwd_partial_ex");
         return FA_OK;
     }
-    int partial_all(size_t o_off, size_t l_off) {
-        if (int st = fa_fwd_partial(q, k, v, ws + o_off, ws + l_off, B, H, L, Lc, d, Lc, dtype, pdtype, s))
+    int fwd_partial(const void* q, const void* k, const void* v, void* o, void* lse, int64_t B, int64_t H,
+                    int64_t Lq, int64_t Lk, int64_t d, int64_t chunk_rows, int dtype, int pdtype, Stream s) {
+        if (int st = fa_fwd_partial(q, k, v, o, lse, B, H, Lq, Lk, d, chunk_rows, dtype, pdtype, s))
             return core_fail(st, "fa_fwd_partial");
         return FA_OK;
     }
-    int fence_to_exchange(int ev) {
-        if (hipError_t he = hipEventRecord(c->ev[ev], s)) return hip_fail(he, "hipEventRecord");
-        if (hipError_t he = hipStreamWaitEvent(c->xstream, c->ev[ev], 0)) return hip_fail(he, "hipStreamWaitEvent");
+    int record(Event e, Stream s) {
+        if (hipError_t he = hipEventRecord(e, s)) return hip_fail(he, "hipEventRecord");
         return FA_OK;
     }
-    int fence_to_compute() {
-        if (hipError_t he = hipEventRecord(c->ev[0], c->xstream)) return hip_fail(he, "hipEventRecord");
-        if (hipError_t he = hipStreamWaitEvent(s, c->ev[0], 0)) return hip_fail(he, "hipStreamWaitEvent");
+    int wait(Stream s, Event e) {
+        if (hipError_t he = hipStreamWaitEvent(s, e, 0)) return hip_fail(he, "hipStreamWaitEvent");
         return FA_OK;
     }
-    // one step of the shifted exchange on the exchange stream: send chunk rank+st to rank+st,
-    // receive chunk rank from rank-st (all ranks' links busy at once, every step a matching)
-    int post_step(int st, int dst, int src, size_t so, size_t ro, size_t sl, size_t rl) {
-        const size_t chunk_o = (size_t)B * H * Lc * d * esize(pdtype);
-        const size_t chunk_l = (size_t)B * H * Lc * lsize(dtype, pdtype);
-        ncclResult_t r = ncclGroupStart();
-        if (r == ncclSuccess) {
-            // (inside a group RCCL only queues; an error here discards the whole group at
-            // ncclGroupEnd, nothing of it is posted)
-            ncclResult_t e = ncclSend(ws + so, chunk_o, ncclUint8, dst, c->nccl, c->xstream);
-            if (e == ncclSuccess) e = ncclRecv(ws + ro, chunk_o, ncclUint8, src, c->nccl, c->xstream);
-            if (e == ncclSuccess) e = ncclSend(ws + sl, chunk_l, ncclUint8, dst, c->nccl, c->xstream);
-            if (e == ncclSuccess) e = ncclRecv(ws + rl, chunk_l, ncclUint8, src, c->nccl, c->xstream);
-            r = ncclGroupEnd();
-            if (e != ncclSuccess) r = e;
-        }
+    // (inside a group RCCL only queues; an error there discards the whole group at
+    // ncclGroupEnd, nothing of it is posted -- so the group is always closed)
+    int group_start() {
+        if (ncclResult_t r = ncclGroupStart()) return rccl_fail(r, "ncclGroupStart");
+        return FA_OK;
+    }
+    int group_end(int first_error, int st, int dst, int src) {
+        const ncclResult_t r = ncclGroupEnd();
+        if (first_error) return first_error;
         if (r != ncclSuccess) {
             char what[96];
             snprintf(what, sizeof what, "exchange step %d (to rank %d, from rank %d)", st, dst, src);
@@ -140,8 +106,16 @@ struct RcclOps {
         }
         return FA_OK;
     }
-    int local_copy(size_t dst_off, size_t src_off, size_t bytes) {
-        if (hipError_t he = hipMemcpyAsync(ws + dst_off, ws + src_off, bytes, hipMemcpyDeviceToDevice, s))
+    int send(const void* p, size_t bytes, int peer, Stream s) {
+        if (ncclResult_t r = ncclSend(p, bytes, ncclUint8, peer, nccl, s)) return rccl_fail(r, "ncclSend");
+        return FA_OK;
+    }
+    int recv(void* p, size_t bytes, int peer, Stream s) {
+        if (ncclResult_t r = ncclRecv(p, bytes, ncclUint8, peer, nccl, s)) return rccl_fail(r, "ncclRecv");
+        return FA_OK;
+    }
+    int copy(void* dst, const void* src, size_t bytes, Stream s) {
+        if (hipError_t he = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s))
             return hip_fail(he, "own chunk copy");
         return FA_OK;
     }
@@ -239,25 +213,17 @@ int fa_fwd_v2_dist(const void* q, const void* k_shard, const void* v_shard, void
     const Layout w = layout(BH, L, d, dtype, partial_dtype);
     char* ws = (char*)workspace;
     hipStream_t s = (hipStream_t)stream;
-    const size_t chunk_o = (size_t)BH * Lc * d * esize(partial_dtype);
-    const size_t chunk_l = (size_t)BH * Lc * lsize(dtype, partial_dtype);
     // pipelined (one partial launch per destination chunk, a q row-range view in place) for
     // bf16 / fp16; fp64 (no strided kernels) computes all chunks in one launch first
     const bool pipelined = dtype != FA_DTYPE_FP64 && world > 1 && d % 8 == 0;
     // The schedule (step pairing, chunk offsets, own-chunk path, failure latch) is
-    // fa_dist_schedule.hpp's run_exchange, exercised on the CPU with an in-process transport
-    // (tests/test_dist_schedule.py); these are its HIP / RCCL operations.
-    fa::dist::Plan plan;
-    plan.world = world;
-    plan.rank = rank;
-    plan.pipelined = pipelined;
-    plan.send_o = w.send_o;
-    plan.send_lse = w.send_lse;
-    plan.recv_o = w.recv_o;
-    plan.recv_lse = w.recv_lse;
-    plan.chunk_o = chunk_o;
-    plan.chunk_l = chunk_l;
-    RcclOps ops{c, ws, q, k_shard, v_shard, B, H, L, Lc, d, dtype, partial_dtype, s};
+    // fa_dist_schedule.hpp's run_exchange; its operations (kernels, events, sends / receives)
+    // are fa_dist_ops.hpp's ExchangeOps over this file's HIP / RCCL primitives.  Both run on
+    // the CPU against simulated ranks (tests/test_dist_schedule.py, tests/test_dist_ops.py).
+    const fa::dist::Plan plan = fa::dist::make_plan(world, rank, pipelined, w, BH, Lc, d, dtype, partial_dtype);
+    HipRcclApi api{c->nccl};
+    fa::dist::ExchangeOps<HipRcclApi> ops{api, c->ev.data(), s, c->xstream, ws, q, k_shard, v_shard,
+                                          B, H, L, Lc, d, dtype, partial_dtype};
     if (int st = fa::dist::run_exchange(plan, ops, c->broken)) return st;
     // combine the W partials of this rank's rows
     void* rows_out = gather && world > 1 ? (void*)(ws + w.gather + rank * (size_t)BH * Lc * d * esize(dtype)) : o;
