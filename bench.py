@@ -227,20 +227,13 @@ def time_step(torch, step, steps, warmup, barrier):
     return wall, ev0.elapsed_time(ev1)
 
 
-def fwd_kernel_name(d, Lk, what, items=None, cus=256):
-    """The kernel a contiguous forward launch runs (fa_fwd.hip launch_one): d = 128 with whole
-    128-key pairs of tiles and at least a query tile (item) per workgroup of a 2-per-CU grid on
-    fa_fwd16_chain_kernel (the chained persistent grid), other whole 64-key tiles at d = 128 on
-    fa_fwd16_kernel (16x16x32 MFMA), everything else on fa_fwd_kernel."""
-    if d == 128 and Lk % 128 == 0 and Lk >= 256 and items is not None and items >= 2 * cus:
-        name = "fa_fwd16_chain_kernel"
-    else:
-        name = "fa_fwd16_kernel" if d == 128 and Lk % 64 == 0 else "fa_fwd_kernel"
-    return f"{name} ({what})"
-
-
-def _cus(torch):
-    return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+def launched(ops, step):
+    """Run `step` once and return the kernels (with their grids) the library reports having
+    launched for it (fa_last_kernels via ops.launched_kernels) -- what ran, as the launcher
+    chose it, not a restatement of its rules."""
+    with ops.launched_kernels() as kl:
+        step()
+    return " + ".join(dict.fromkeys(kl)) if kl else None
 
 
 def clock_settle(torch, step, seconds):
@@ -270,14 +263,15 @@ def c5_step(torch, fdist, dev, world, rank, impl="torch"):
 
         def step():
             fdist.splitkv_attention_native(q, k, v, comm)
-        kernel = (fwd_kernel_name(d, hi - lo, "partial, one launch per destination chunk") +
-                  " + RCCL send/recv on the exchange stream + fa_combine_kernel (C ABI fa_fwd_v2_dist)")
+        kernel = ("fa_fwd_partial_ex per destination chunk + RCCL send/recv on the exchange stream + "
+                  "fa_combine (C ABI fa_fwd_v2_dist; its launches are internal to libfa_mi355x_dist.so)")
     else:
         def step():
             fdist.splitkv_attention(q, k, v)
-        kernel = (fwd_kernel_name(d, hi - lo, "partial, one launch per destination chunk") +
-                  " + pipelined RCCL send/recv + fa_combine_kernel" if world > 1
-                  else fwd_kernel_name(d, hi - lo, "partial") + " + fa_combine_kernel")
+        from exploring_flash_attention_amd import ops
+        kernel = launched(ops, step)
+        if world > 1:
+            kernel = f"{kernel} (pipelined RCCL send/recv between the partial chunks and the combine)"
     return step, kernel, flops(B, H, L, d, Lk=hi - lo)
 
 
@@ -367,7 +361,7 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
         elif fn == "tiled_d":
             def st():
                 ops.attention_tiled_d(qq, kk, vv, 128, 128)
-            rec.update(d_tile_qk=128, d_tile_v=128, kernel=f"fa_fwd_dt_kernel (d = {d})")
+            rec.update(d_tile_qk=128, d_tile_v=128)
         else:
             if grp == "all":  # every key block of a query tile on one workgroup: no split
                 grp = ops.v2_split_plan(B, H, L, d, kvt, qq.dtype)[0]
@@ -386,6 +380,7 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
         # low-power one boosts it, a hot one holds it down) otherwise carries into this window
         # (C4 read 1.84 ms after the d = 512 shape and 1.74 ms for the same kernel and grid as
         # c4_splitkv_auto; profiles/r04/bench_driver_cmd_g.json)
+        rec["kernel"] = launched(ops, st)
         clock_settle(torch, st, EXTRA_SETTLE_S)
         _, ems = time_step(torch, st, n, max(3, n // 3), barrier)
         ms = ems / n
@@ -603,19 +598,13 @@ def main():
         if cfg["variant"] == "v1":
             def step():
                 ops.attention_v1(q, k, v, out=out)
-            kernel = fwd_kernel_name(d, L, "final", items=B * H * (L // 128), cus=_cus(torch))
         else:
             nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
 
             def step():
                 ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
-            _, _, ppt = ops.v2_split_plan(B, H, L, d, cfg["kvtpb"], q.dtype)
-            kernel = (fwd_kernel_name(d, L, "fused split-KV, in-kernel combine", items=B * H * (L // 128) * ppt,
-                                      cus=_cus(torch)) if ppt > 1
-                      else fwd_kernel_name(d, L, "final: the library groups every key block of a query tile "
-                                                 "on one workgroup, fa_fwd_v2_split_plan",
-                                           items=B * H * (L // 128), cus=_cus(torch)))
+        kernel = launched(ops, step)
         # Clock settle, immediately before the headline's --warmup (after the extras, whose
         # last shapes are small): the chip needs ~50 ms of back-to-back work before its clock
         # holds, so the headline's own step runs untimed for

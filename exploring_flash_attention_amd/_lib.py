@@ -35,6 +35,7 @@ _PI = ctypes.POINTER(ctypes.c_int)
 SIGNATURES = {
     "fa_version": (_I, []),
     "fa_last_error": (ctypes.c_char_p, []),
+    "fa_last_kernels": (ctypes.c_char_p, []),
     "fa_kernel_geometry": (_I, [_I64, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                 ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "fa_fwd_v1": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _P]),
@@ -101,6 +102,12 @@ def check(status):
     if status in (FA_ERR_INVALID_ARG, FA_ERR_UNSUPPORTED, FA_ERR_WORKSPACE):
         raise FaArgumentError(status, msg)
     raise FaError(status, msg)
+
+
+def last_kernels():
+    """The kernels (with their grids) the last launching C-ABI call of this thread enqueued,
+    as the library's launcher chose them (fa_last_kernels)."""
+    return lib().fa_last_kernels().decode(errors="replace")
 
 
 def geometry(d, dtype=FA_DTYPE_BF16):

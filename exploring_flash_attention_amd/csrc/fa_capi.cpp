@@ -16,12 +16,14 @@
 #include "fa_internal.hpp"
 
 namespace fa {
-// Compute units of the current device, queried once per device (the split planner runs on
-// every fa_fwd_v2 call).  No device (CPU-only tests): the MI355X's 256.
-int device_cus() {
+// Compute units of the device that owns `s` (the current device for the null stream), queried
+// once per device (the split planner runs on every fa_fwd_v2 call).  No device (CPU-only
+// tests): the MI355X's 256.
+int device_cus(hipStream_t s) {
     static std::atomic<int> cached[64];
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    hipError_t he = s ? hipStreamGetDevice(s, &dev) : hipGetDevice(&dev);
+    if (he != hipSuccess || dev < 0 || dev >= 64) {
         (void)hipGetLastError();
         return 256;
     }
@@ -34,11 +36,21 @@ int device_cus() {
     cached[dev].store(n, std::memory_order_relaxed);
     return n;
 }
+
+// fa_last_kernels(): what the last launching call of this thread enqueued
+thread_local std::string g_kernels;
+void kernels_begin() { g_kernels.clear(); }
+void note_kernel(const char* name, int64_t grid) {
+    if (!g_kernels.empty()) g_kernels += " + ";
+    g_kernels += name;
+    g_kernels += " [grid " + std::to_string(grid) + "]";
+}
 }  // namespace fa
 
 namespace {
 
 using fa::device_cus;
+using fa::kernels_begin;
 
 thread_local std::string g_err;
 
@@ -376,6 +388,8 @@ int fa_version(void) { return (FA_MI355X_VERSION_MAJOR << 16) | (FA_MI355X_VERSI
 
 const char* fa_last_error(void) { return g_err.c_str(); }
 
+const char* fa_last_kernels(void) { return fa::g_kernels.c_str(); }
+
 int fa_kernel_geometry(int64_t d, int dtype, int* bq, int* bk, int* threads, int* lds_bytes) {
     fa::Elem e;
     if (int st = check_dtype(dtype, &e)) return st;
@@ -432,6 +446,7 @@ int fa_fwd_v1_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     fa::FwdArgs a = base_args(q, k, v, o, B * H, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
     if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
+    kernels_begin();
     if (hipError_t he = launch_final(e, (int)d, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v1 launch");
     return ok();
@@ -455,6 +470,7 @@ int fa_fwd_v1_tiled_d_scaled(const void* q, const void* k, const void* v, void* 
     if (int st = apply_scale(a, softmax_scale)) return st;
     // d <= 256: one tile holds a whole row -- the fused kernel (its QK^T accumulates 32-column
     // k-steps, its O^T stays in VGPRs); d = 384 / 512: the d-tiled kernels, tiles honoured
+    kernels_begin();
     const hipError_t he = wide_d(d) ? launch_wide(e, (int)d, a, d_tile_qk, d_tile_v, (hipStream_t)stream)
                                     : launch_final(e, (int)d, a, (hipStream_t)stream);
     if (he) return hip_fail(he, "fa_fwd_v1_tiled_d launch");
@@ -541,6 +557,7 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     fa::FwdArgs a = base_args(q, k, v, o, BH, L, L, d, e);
     if (int st = apply_scale(a, softmax_scale)) return st;
     if (int st = apply_strides(a, e, B, H, L, d, q_strides, kv_strides, o_strides)) return st;
+    kernels_begin();
     if (ns == 1) {  // one partial workgroup per query tile: nothing to combine
         const hipError_t he = wide_d(d) ? launch_wide(e, (int)d, a, d_tile_qk, d_tile_v, (hipStream_t)stream)
                                         : launch_final(e, (int)d, a, (hipStream_t)stream);
@@ -617,6 +634,7 @@ int fa_fwd_partial_ex(const void* q, const void* k, const void* v, void* o_part,
     a.chunk_rows = chunk_rows;
     a.split_stride = 0;
     if (int st = apply_strides(a, e, B, H, Lq, d, q_strides, nullptr, nullptr, Lk)) return st;
+    kernels_begin();
     if (hipError_t he = e == fa::Elem::F64
                             ? fa::launch_fwd64((int)d, fa::kPartial, a, (hipStream_t)stream)
                             : fa::launch_fwd(e, pe, (int)d, fa::kPartial, a, (hipStream_t)stream))
@@ -642,6 +660,7 @@ int fa_combine(const void* o_part, const void* lse, void* o, int64_t num_splits,
     fa::CombineArgs c{};
     c.o_part = o_part; c.lse = (const float*)lse; c.lse64 = (const double*)lse; c.o = o;
     c.rows = B * H * L; c.nsplit = (int)num_splits;
+    kernels_begin();
     if (hipError_t he = e == fa::Elem::F64 ? fa::launch_combine64((int)d, c, (hipStream_t)stream)
                                            : fa::launch_combine(e, pe, (int)d, c, (hipStream_t)stream))
         return hip_fail(he, "fa_combine launch");

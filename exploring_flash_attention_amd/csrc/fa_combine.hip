@@ -83,6 +83,7 @@ template <typename T, typename PT>
 static hipError_t launch_c(int d, const CombineArgs& a, hipStream_t s) {
     const int64_t threads = a.rows * (d / 8);
     const dim3 grid((unsigned)((threads + 255) / 256));
+    note_kernel("fa_combine_kernel", grid.x);
     switch (d) {
         case 32: hipLaunchKernelGGL((fa_combine_kernel<T, PT, 32>), grid, dim3(256), 0, s, a); break;
         case 64: hipLaunchKernelGGL((fa_combine_kernel<T, PT, 64>), grid, dim3(256), 0, s, a); break;

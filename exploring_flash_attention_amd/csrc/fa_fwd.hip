@@ -27,21 +27,24 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
             // scaled fp16 partials, each tile combined by its own workgroup): an even number >= 4
             // of 64-key tiles per key block, whole query tiles, and at least one query tile per
             // workgroup of a 2-per-CU grid
-            const int64_t grid = 2 * (int64_t)device_cus() / 8 * 8;
+            const int64_t grid = 2 * (int64_t)device_cus(s) / 8 * 8;
             const int64_t kvi = MODE == kFused ? a.kv_per_split : a.Lk;
             const int64_t tiles = (int64_t)a.nqt * a.BH;
             if (FA_CHAIN && kvi % 128 == 0 && kvi >= 256 && a.Lk % kvi == 0 && a.Lq % kBQ == 0 &&
                 (MODE == kFused || a.nsplit == 1) && tiles >= grid && grid >= 8 && nblk < (int64_t)1 << 31) {
+                note_kernel(MODE == kFinal ? "fa_fwd16_chain_kernel<final>" : "fa_fwd16_chain_kernel<fused walk>", grid);
                 hipLaunchKernelGGL((fa_fwd16_chain_kernel<T, MODE>), dim3((unsigned)grid), dim3(kThreads),
                                    lds, s, a, (int)tiles);
                 return hipGetLastError();
             }
         }
         if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {  // no key tail in any split
+            note_kernel(kernel_label(true, MODE, false), nblk);
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();
         }
     }
+    note_kernel(kernel_label(false, MODE, false), nblk);
     if (a.Lk % bk_for(D) || !(kNoTailMask & d_bit(D)))
         hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads),
                            lds, s, a);

@@ -81,8 +81,9 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
     char* const vring = smem + 2 * TILEB;
 
     // this workgroup's items: group x = blockIdx % 8 owns xcd_remap's contiguous range
-    const int nl = gridDim.x >> 3, x = blockIdx.x & 7, l = blockIdx.x >> 3;
+    const int x = blockIdx.x & 7;
     const int iq = nitems >> 3, ir = nitems & 7;
+    const int nl = gridDim.x >> 3, l = blockIdx.x >> 3;
     const int gstart = x < ir ? x * (iq + 1) : ir * (iq + 1) + (x - ir) * iq;
     const int gcnt = iq + (x < ir ? 1 : 0);
     const int nmine = l < gcnt ? (gcnt - l + nl - 1) / nl : 0;
@@ -657,7 +658,12 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
         Epi prev_ep = enone;  // where the previous item's O goes
         for (int j = 0;; ++j) {
             const bool more = j + 1 < nmine;
-            const Item nxt = item(more ? j + 1 : j);
+            // after the last item the "next" Q^T load is an empty range too (q_rows = 0: the
+            // loads return zeros and move no bytes) -- reloading the current tile's Q^T there
+            // cost 32 KiB of L2 misses per workgroup, +17 MB (+6 %) of reads at C3 in the round-5
+            // kernel (profiles/r06/pmc_fetch.txt), and its latency sat on the workgroup's tail
+            Item nxt = item(more ? j + 1 : j);
+            nxt.q_rows = more ? nxt.q_rows : 0;
             // t = 0, 1 (step 0 stores the previous item's O)
             step(C0{}, std::integral_constant<int, 1 | 4 | 32>{}, sa, sb, mx, tile_rsrc(cur.k, 2), tile_rsrc(cur.v, 1),
                  nxt, prev_ep);

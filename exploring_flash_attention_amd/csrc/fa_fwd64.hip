@@ -261,6 +261,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd64_dt_kernel(FwdArgs a) {
 
 hipError_t launch_fwd64_dtiled(int d, const FwdArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
+    note_kernel("fa_fwd64_dt_kernel", grid.x);
     if (d == 384) hipLaunchKernelGGL((fa_fwd64_dt_kernel<384>), grid, dim3(256), 0, s, a);
     else if (d == 512) hipLaunchKernelGGL((fa_fwd64_dt_kernel<512>), grid, dim3(256), 0, s, a);
     else return hipErrorInvalidValue;
@@ -291,6 +292,7 @@ int fwd64_keys_per_tile() { return kBK64; }
 hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((int64_t)a.nqt * a.nsplit * a.BH));
     auto go = [&](auto kern) {
+        note_kernel(mode == kFinal ? "fa_fwd64_kernel<final>" : "fa_fwd64_kernel<partial>", grid.x);
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a);
         return hipGetLastError();
     };
@@ -314,6 +316,7 @@ hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s) {
 
 hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((a.rows * d + 255) / 256));
+    note_kernel("fa_combine64_kernel", grid.x);
     switch (d) {
         case 32: hipLaunchKernelGGL((fa_combine64_kernel<32>), grid, dim3(256), 0, s, a); break;
         case 64: hipLaunchKernelGGL((fa_combine64_kernel<64>), grid, dim3(256), 0, s, a); break;

@@ -349,6 +349,7 @@ void dtiled_geometry(Elem, int d, int* rows, int* threads, int* lds) {
 template <typename T, int D>
 static hipError_t launch_dt(const FwdArgs& a, const dim3& grid, int lds, hipStream_t s) {
     auto go = [&](auto kern) {
+        note_kernel("fa_fwd_dt_kernel", grid.x);
         hipLaunchKernelGGL(kern, grid, dim3(kDtWaves * 64), lds, s, a);
         return hipGetLastError();
     };

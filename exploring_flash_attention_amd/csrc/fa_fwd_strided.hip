@@ -19,10 +19,12 @@ static hipError_t launch_strided_one(const FwdArgs& a, hipStream_t s) {
     // contiguous launch (round 4; the 32x32x16 kernel below sums in another order)
     if constexpr (D == 128) {
         if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {
+            note_kernel(kernel_label(true, MODE, true), nblk);
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE, true>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);
             return hipGetLastError();
         }
     }
+    note_kernel(kernel_label(false, MODE, true), nblk);
     if (a.Lk % bk_for(D))
         hipLaunchKernelGGL((fa_fwd_kernel<T, PT, D, MODE, true, true>), dim3((unsigned)nblk), dim3(kThreads),
                            lds, s, a);

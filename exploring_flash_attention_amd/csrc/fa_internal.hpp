@@ -132,8 +132,25 @@ hipError_t launch_combine(Elem t, Elem pt, int d, const CombineArgs& a, hipStrea
 // the strided instantiations (fa_fwd_strided.hip); launch_fwd forwards there when a.strided
 hipError_t launch_fwd_strided(Elem t, Elem pt, int d, Mode mode, const FwdArgs& a, hipStream_t s);
 int fwd_lds_bytes(int d);
-// compute units of the current device (fa_capi.cpp; 256 without a device)
-int device_cus();
+// compute units of the device that owns `s` (the current device for the null stream;
+// fa_capi.cpp; 256 without a device)
+int device_cus(hipStream_t s = nullptr);
+// The kernels a C-ABI call enqueued, for fa_last_kernels() (fa_capi.cpp): every launcher
+// names the kernel it picked and its grid, so callers (bench.py) report what ran instead of
+// restating the launch rules.
+void note_kernel(const char* name, int64_t grid);
+// the forward kernels' labels (string literals: nothing allocated on the launch path)
+inline const char* kernel_label(bool k16, int mode, bool strided) {
+    static const char* const names[2][3][2] = {
+        {{"fa_fwd_kernel<final>", "fa_fwd_kernel<final, strided>"},
+         {"fa_fwd_kernel<partial>", "fa_fwd_kernel<partial, strided>"},
+         {"fa_fwd_kernel<fused split, in-kernel combine>", "fa_fwd_kernel<fused split, in-kernel combine, strided>"}},
+        {{"fa_fwd16_kernel<final>", "fa_fwd16_kernel<final, strided>"},
+         {"fa_fwd16_kernel<partial>", "fa_fwd16_kernel<partial, strided>"},
+         {"fa_fwd16_kernel<fused split, in-kernel combine>",
+          "fa_fwd16_kernel<fused split, in-kernel combine, strided>"}}};
+    return names[k16 ? 1 : 0][mode < 0 || mode > 2 ? 0 : mode][strided ? 1 : 0];
+}
 // fp64 mode (fa_fwd64.hip): 64 query rows x 16-key tiles; final or row-layout partial
 hipError_t launch_fwd64(int d, Mode mode, const FwdArgs& a, hipStream_t s);
 hipError_t launch_combine64(int d, const CombineArgs& a, hipStream_t s);

@@ -14,7 +14,9 @@ Reference launchers these replace (tyler-utah/exploring_flash_attention):
   attention_partial  partial_attention_kernel, flash_attention_v2/CUDA/flash_attention_v2.h:243
   combine            reduction_kernel,         flash_attention_v2/CUDA/flash_attention_v2.h:356
 """
+import contextlib
 import ctypes
+import threading
 
 import torch
 
@@ -30,6 +32,31 @@ _DTYPES = {torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16, torch.fl
 PARTIAL_FP16_SCALED = "fp16_scaled"
 _PDTYPES = {torch.float32: FA_DTYPE_FP32, torch.bfloat16: FA_DTYPE_BF16, torch.float16: FA_DTYPE_FP16,
             torch.float64: FA_DTYPE_FP64, PARTIAL_FP16_SCALED: FA_DTYPE_FP16_SCALED}
+
+
+_klog = threading.local()
+
+
+def _launched(status):
+    """check() for a call that launches kernels; inside launched_kernels() also records what
+    the library's launcher enqueued (fa_last_kernels)."""
+    check(status)
+    log = getattr(_klog, "log", None)
+    if log is not None:
+        log.append(_lib.last_kernels())
+
+
+@contextlib.contextmanager
+def launched_kernels():
+    """Collect, in call order, the kernels (with grids) every operator of this module launches
+    on this thread inside the block -- the library's own report (fa_last_kernels), so a caller
+    such as bench.py names what ran instead of restating the launch rules."""
+    prev = getattr(_klog, "log", None)
+    _klog.log = []
+    try:
+        yield _klog.log
+    finally:
+        _klog.log = prev
 
 
 def _default_pdtype(dtype, partial_dtype, fused=False):
@@ -165,14 +192,14 @@ def attention_v1(q, k, v, out=None):
         return _via_contiguous(attention_v1, q, k, v, o)
     if D == d:
         if st is None:
-            check(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
+            _launched(lib().fa_fwd_v1(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, _DTYPES[q.dtype], _stream(q)))
         else:
-            check(lib().fa_fwd_v1_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, st[0], st[1], st[2],
+            _launched(lib().fa_fwd_v1_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, st[0], st[1], st[2],
                                      1.0 / d ** 0.5, _DTYPES[q.dtype], _stream(q)))
         return o
     qp, kp, vp = (_pad_d(t, D) for t in (q, k, v))
     op = torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
-    check(lib().fa_fwd_v1_scaled(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, 1.0 / d ** 0.5,
+    _launched(lib().fa_fwd_v1_scaled(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, 1.0 / d ** 0.5,
                                  _DTYPES[q.dtype], _stream(q)))
     return _unpad_into(op, o, d)
 
@@ -209,7 +236,7 @@ def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
             # padded head dims and strided views run on fa_fwd_v1's paths (the same kernel)
             return attention_v1(q, k, v, out=out)
         o = _out(out, q)
-        check(lib().fa_fwd_v1_tiled_d(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+        _launched(lib().fa_fwd_v1_tiled_d(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
                                       int(d_tile_v), _DTYPES[q.dtype], _stream(q)))
         return o
     o = _out(out, q, strided=True)
@@ -217,7 +244,7 @@ def attention_tiled_d(q, k, v, d_tile_qk=None, d_tile_v=None, out=None):
         return o
     qc, kc, vc = (_pad_d(t.contiguous(), D) for t in (q, k, v))
     oc = o if D == d and o.is_contiguous() else torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
-    check(lib().fa_fwd_v1_tiled_d_scaled(_ptr(qc), _ptr(kc), _ptr(vc), _ptr(oc), B, H, L, D, int(d_tile_qk),
+    _launched(lib().fa_fwd_v1_tiled_d_scaled(_ptr(qc), _ptr(kc), _ptr(vc), _ptr(oc), B, H, L, D, int(d_tile_qk),
                                          int(d_tile_v), 1.0 / d ** 0.5, _DTYPES[q.dtype], _stream(q)))
     if oc is not o:
         o.copy_(oc[..., :d])
@@ -304,7 +331,7 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
     wsb = workspace.numel() * workspace.element_size()
     if D == d:
         sq, skv, so = (None, None, None) if st is None else st
-        check(lib().fa_fwd_v2_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
+        _launched(lib().fa_fwd_v2_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, L, d, int(d_tile_qk),
                                  int(d_tile_v), int(kv_tiles_per_block), bpw, _ptr(workspace), wsb, sq, skv,
                                  so, 1.0 / d ** 0.5, _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
         return o
@@ -313,7 +340,7 @@ def attention_v2(q, k, v, kv_tiles_per_block=4, d_tile_qk=None, d_tile_v=None, p
             raise _lib.FaArgumentError(1, f"{name}={int(t)} must satisfy 0 < {name} <= d={d}")
     qp, kp, vp = (_pad_d(t, D) for t in (q, k, v))
     op = torch.empty((B, H, L, D), dtype=q.dtype, device=q.device)
-    check(lib().fa_fwd_v2_ex(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, int(d_tile_qk),
+    _launched(lib().fa_fwd_v2_ex(_ptr(qp), _ptr(kp), _ptr(vp), _ptr(op), B, H, L, D, int(d_tile_qk),
                              int(d_tile_v), int(kv_tiles_per_block), bpw, _ptr(workspace), wsb, None, None, None,
                              1.0 / d ** 0.5, _DTYPES[q.dtype], _PDTYPES[pd], _stream(q)))
     return _unpad_into(op, o, d)
@@ -351,10 +378,10 @@ def attention_partial(q, k, v, chunk_rows=None, partial_dtype=None, o_part=None,
     o_part = _out(o_part, q, (nch, B * H, cr, d), torch.float16 if scaled else partial_dtype)
     lse = _out(lse, q, (nch, B * H, cr, 2) if scaled else (nch, B * H, cr), lse_dtype)
     if qst is None:
-        check(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
+        _launched(lib().fa_fwd_partial(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
                                    cr, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
     else:
-        check(lib().fa_fwd_partial_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
+        _launched(lib().fa_fwd_partial_ex(_ptr(q), _ptr(k), _ptr(v), _ptr(o_part), _ptr(lse), B, H, Lq, Lk, d,
                                       cr, qst, _DTYPES[q.dtype], _PDTYPES[partial_dtype], _stream(q)))
     return o_part, lse
 
@@ -376,7 +403,7 @@ def combine(o_part, lse, B, H, dtype, out=None):
         raise ValueError(f"scaled partials (lse [..., 2]) are fp16, got {o_part.dtype}")
     o = _out(out, o_part, (B, H, L, d), dtype)
     pd = PARTIAL_FP16_SCALED if scaled else o_part.dtype
-    check(lib().fa_combine(_ptr(o_part), _ptr(lse), _ptr(o), S, B, H, L, d, _DTYPES[dtype],
+    _launched(lib().fa_combine(_ptr(o_part), _ptr(lse), _ptr(o), S, B, H, L, d, _DTYPES[dtype],
                            _PDTYPES[pd], _stream(o_part)))
     return o
 

@@ -78,15 +78,26 @@ typedef enum fa_dtype {
  *   0.2 -- fa_fwd_v2_ex and fa_fwd_v2_split_plan gained the int blocks_per_workgroup argument
  *          (inserted before workspace / dtype), fa_fwd_v2_workspace_size_ex was added;
  *   0.3 -- head dims 384 and 512 (the d-tiled kernels: fa_fwd_v1, fa_fwd_v1_tiled_d, and
- *          fa_fwd_v2 unsplit), fa_fwd_v1_tiled_d_scaled added.
+ *          fa_fwd_v2 unsplit), fa_fwd_v1_tiled_d_scaled added;
+ *   0.4 -- fa_last_kernels added (no signature changed).
  * fa_version() returns the library's (major << 16) | (minor << 8) | patch; check it against
  * these macros at load time. */
 #define FA_MI355X_VERSION_MAJOR 0
-#define FA_MI355X_VERSION_MINOR 3
+#define FA_MI355X_VERSION_MINOR 4
 int fa_version(void);
 
 /* Thread-local message describing the last non-FA_OK status on this thread. */
 const char* fa_last_error(void);
+
+/* Thread-local description of the kernels the last launching call on this thread enqueued
+ * (fa_fwd_v1*, fa_fwd_v1_tiled_d*, fa_fwd_v2*, fa_fwd_partial*, fa_combine), each with its
+ * grid, joined by " + ", e.g. "fa_fwd16_chain_kernel<final> [grid 512]".  Valid after an FA_OK
+ * return; the reference's launchers have no equivalent (a profiling aid: which of the
+ * library's kernels and grids served the call, as the launcher chose them).  The grids of the
+ * d = 128 persistent kernels are sized from the compute units of the device that owns
+ * `stream`; the split-KV plan (fa_fwd_v2_split_plan, the workspace size) from the current
+ * device's -- call them with the stream's device current. */
+const char* fa_last_kernels(void);
 
 /* Geometry the library uses for (d, dtype): query rows per workgroup (*bq),
  * keys per KV tile (*bk), threads per workgroup (*threads), LDS bytes per workgroup

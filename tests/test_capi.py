@@ -39,11 +39,12 @@ def test_exports_are_c_symbols_not_mangled():
 
 
 def test_version_and_geometry():
-    # ABI 0.3 (include/fa_mi355x.h FA_MI355X_VERSION_*): blocks_per_workgroup in 0.2, d = 384 / 512
+    # ABI 0.4 (include/fa_mi355x.h FA_MI355X_VERSION_*): blocks_per_workgroup in 0.2, d = 384 / 512
+    # in 0.3, fa_last_kernels in 0.4
     hdr = open(os.path.join(ROOT, "include", "fa_mi355x.h")).read()
     major = int(re.search(r"#define FA_MI355X_VERSION_MAJOR (\d+)", hdr).group(1))
     minor = int(re.search(r"#define FA_MI355X_VERSION_MINOR (\d+)", hdr).group(1))
-    assert L.lib().fa_version() == (major << 16) | (minor << 8) == 0x000300
+    assert L.lib().fa_version() == (major << 16) | (minor << 8) == 0x000400
     bq, bk, threads, lds = L.geometry(128)
     assert (bq, bk, threads) == (128, 64, 256)
     assert lds == 2 * 2 * 64 * 128 * 2

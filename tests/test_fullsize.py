@@ -268,3 +268,36 @@ def test_long_sequence_split_paths(gpu, shape, kvt, group, partials):
     qs = q[:, :, rows].cpu().double().numpy()
     ref = attention_fp64(qs, k.cpu().double().numpy(), v.cpu().double().numpy())
     _gate(o1[:, :, rows].cpu(), ref, torch.bfloat16, label=f"long split B{b} H{h} L{L} ({partials} partials)")
+
+
+def test_launched_kernels_reported(gpu):
+    """fa_last_kernels (ops.launched_kernels): each operator reports the kernel and grid the
+    library's launcher picked -- the chained persistent grid of exactly 2 workgroups per CU at
+    C3-like shapes, the one-shot grid below it, the 32x32x16 kernel for d = 32 and key tails,
+    the fused split-KV kernel, the d-tiled kernel, and partial + combine."""
+    from exploring_flash_attention_amd import ops
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    grid = 2 * cus // 8 * 8
+
+    def run(fn, *shape, dtype=torch.bfloat16):
+        B, H, L, d = shape
+        q, k, v = (torch.randn(B, H, L, d, device=gpu, dtype=dtype) for _ in range(3))
+        with ops.launched_kernels() as kl:
+            fn(q, k, v)
+        torch.cuda.synchronize()
+        return kl
+
+    tiles = grid  # a C3-like shape with exactly one query tile per workgroup of the grid
+    assert run(ops.attention_v1, 1, tiles // 8, 1024, 128) == [f"fa_fwd16_chain_kernel<final> [grid {grid}]"]
+    assert run(ops.attention_v1, 1, 2, 1024, 128) == ["fa_fwd16_kernel<final> [grid 16]"]
+    assert run(ops.attention_v1, 2, 2, 1024, 32) == ["fa_fwd_kernel<final> [grid 32]"]
+    assert run(ops.attention_v1, 1, 2, 1000, 128) == ["fa_fwd_kernel<final> [grid 16]"]
+    assert run(lambda q, k, v: ops.attention_tiled_d(q, k, v, 64, 64), 1, 2, 256, 384) == ["fa_fwd_dt_kernel [grid 8]"]
+    kl = run(lambda q, k, v: ops.attention_v2(q, k, v, 4), 1, 2, 4096, 128)
+    assert len(kl) == 1 and kl[0].startswith("fa_fwd16_kernel<fused split, in-kernel combine> [grid ")
+    with ops.launched_kernels() as kl:
+        q, k, v = (torch.randn(1, 2, 512, 128, device=gpu, dtype=torch.bfloat16) for _ in range(3))
+        o_part, lse = ops.attention_partial(q, k, v)
+        ops.combine(o_part, lse, 1, 2, torch.bfloat16)
+    torch.cuda.synchronize()
+    assert kl[0] == "fa_fwd16_kernel<partial> [grid 8]" and kl[1].startswith("fa_combine_kernel [grid ")
