@@ -367,11 +367,13 @@ def single_gpu_extras(torch, ops, dev, barrier, names=None):
                 grp = ops.v2_split_plan(B, H, L, d, kvt, qq.dtype)[0]
             nb, _ = ops.v2_workspace_bytes(B, H, L, d, kvt, qq.dtype, blocks_per_workgroup=grp)
             plan = ops.v2_split_plan(B, H, L, d, kvt, qq.dtype, blocks_per_workgroup=grp)
-            wsx = torch.empty(nb, dtype=torch.uint8, device=dev)
+            # zeroed once; every launch leaves its counters zero (ops.attention_v2 workspace_zeroed)
+            wsx = torch.zeros(nb, dtype=torch.uint8, device=dev)
             oo = torch.empty_like(qq)
 
             def st():
-                ops.attention_v2(qq, kk, vv, kvt, out=oo, workspace=wsx, blocks_per_workgroup=grp)
+                ops.attention_v2(qq, kk, vv, kvt, out=oo, workspace=wsx, blocks_per_workgroup=grp,
+                                 workspace_zeroed=True)
             rec.update(kv_tiles_per_block=kvt, key_blocks=plan[0], blocks_per_workgroup=plan[1],
                        partials_per_tile=plan[2], workspace_bytes=nb)
         f = flops(B, H, L, d)
@@ -600,10 +602,10 @@ def main():
                 ops.attention_v1(q, k, v, out=out)
         else:
             nbytes, _ = ops.v2_workspace_bytes(B, H, L, d, cfg["kvtpb"], q.dtype)
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
 
             def step():
-                ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws)
+                ops.attention_v2(q, k, v, cfg["kvtpb"], out=out, workspace=ws, workspace_zeroed=True)
         kernel = launched(ops, step)
         # Clock settle, immediately before the headline's --warmup (after the extras, whose
         # last shapes are small): the chip needs ~50 ms of back-to-back work before its clock

@@ -25,6 +25,7 @@ FA_DTYPE_FP16_SCALED = 4  # split-KV partials: fp16 scaled per row by a power of
 
 FA_KV_TILES_AUTO = -1  # kv_tiles_per_block: split chosen from the device's occupancy
 FA_BLOCKS_PER_WG_AUTO = 0  # blocks_per_workgroup: the library groups the key blocks itself
+FA_V2_COUNTERS_ZERO = 1  # fa_fwd_v2_ex2: the caller vouches that the workspace counters are zero
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -54,6 +55,8 @@ SIGNATURES = {
                               ctypes.c_double, _I, _I, _P]),
     "fa_fwd_v2_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _P, ctypes.c_size_t,
                           _P, _P, _P, ctypes.c_double, _I, _I, _P]),
+    "fa_fwd_v2_ex2": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _P, ctypes.c_size_t,
+                           _P, _P, _P, ctypes.c_double, _I, _I, ctypes.c_uint, _P]),
     "fa_fwd_partial": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
     "fa_fwd_partial_ex": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _I, _I, _P]),
     "fa_combine": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),

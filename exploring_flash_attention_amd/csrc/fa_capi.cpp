@@ -533,6 +533,17 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
                  int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block, int blocks_per_workgroup,
                  void* workspace, size_t workspace_bytes, const int64_t* q_strides, const int64_t* kv_strides,
                  const int64_t* o_strides, double softmax_scale, int dtype, int partial_dtype, void* stream) {
+    return fa_fwd_v2_ex2(q, k, v, o, B, H, L, d, d_tile_qk, d_tile_v, kv_tiles_per_block, blocks_per_workgroup,
+                         workspace, workspace_bytes, q_strides, kv_strides, o_strides, softmax_scale, dtype,
+                         partial_dtype, 0u, stream);
+}
+
+int fa_fwd_v2_ex2(const void* q, const void* k, const void* v, void* o, int64_t B, int64_t H, int64_t L,
+                  int64_t d, int d_tile_qk, int d_tile_v, int kv_tiles_per_block, int blocks_per_workgroup,
+                  void* workspace, size_t workspace_bytes, const int64_t* q_strides, const int64_t* kv_strides,
+                  const int64_t* o_strides, double softmax_scale, int dtype, int partial_dtype, unsigned flags,
+                  void* stream) {
+    if (flags & ~(unsigned)FA_V2_COUNTERS_ZERO) return fail(FA_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
     fa::Elem e, pe;
     if (int st = check_shape(B, H, L, d, true)) return st;
     if (int st = check_dtype(dtype, &e)) return st;
@@ -595,9 +606,13 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o, int64_t B
     a.o_final = o;
     // the kernel leaves every counter at zero; clearing them here makes a call that follows
     // an aborted one (or a fresh workspace) safe
-    if (hipError_t he = hipMemsetAsync(a.counters, 0, (size_t)w.ngroups * sizeof(unsigned),
-                                       (hipStream_t)stream))
-        return hip_fail(he, "fa_fwd_v2 counter reset");
+    // ... unless the caller vouches for them (FA_V2_COUNTERS_ZERO: a zeroed workspace, or one
+    // only this function has used since): the reset is a dispatch of its own, 1.6-1.8 us per
+    // call (B1 H2 L4096: 27.1 -> 25.3 us, B1 H1 L16384: 127.1 -> 125.5 us; profiles/r06/ab_*_memset.txt)
+    if (!(flags & FA_V2_COUNTERS_ZERO))
+        if (hipError_t he = hipMemsetAsync(a.counters, 0, (size_t)w.ngroups * sizeof(unsigned),
+                                           (hipStream_t)stream))
+            return hip_fail(he, "fa_fwd_v2 counter reset");
     if (hipError_t he = fa::launch_fwd(e, pe, (int)d, fa::kFused, a, (hipStream_t)stream))
         return hip_fail(he, "fa_fwd_v2 launch");
     return ok();

@@ -586,7 +586,13 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
         if (tid == 0) {
             if (af) {
                 const unsigned want = (unsigned)(a.nsplit - 1) << 16;
-                while ((__hip_atomic_load(a.counters + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffff0000u) != want)
+                // (bounded: the others have arrived, so their completions come within
+                // microseconds; a counter that was not zero at the launch -- a caller's broken
+                // FA_V2_COUNTERS_ZERO promise -- ends in a wrong O after ~2^22 polls, not a hang)
+                for (int it = 0; it < (1 << 22) &&
+                                 (__hip_atomic_load(a.counters + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                                  0xffff0000u) != want;
+                     ++it)
                     __builtin_amdgcn_s_sleep(1);
             }
             a.counters[grp] = 0;  // leave the counter zero for the next launch

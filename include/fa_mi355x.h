@@ -79,7 +79,7 @@ typedef enum fa_dtype {
  *          (inserted before workspace / dtype), fa_fwd_v2_workspace_size_ex was added;
  *   0.3 -- head dims 384 and 512 (the d-tiled kernels: fa_fwd_v1, fa_fwd_v1_tiled_d, and
  *          fa_fwd_v2 unsplit), fa_fwd_v1_tiled_d_scaled added;
- *   0.4 -- fa_last_kernels added (no signature changed).
+ *   0.4 -- fa_last_kernels and fa_fwd_v2_ex2 (FA_V2_COUNTERS_ZERO) added (no signature changed).
  * fa_version() returns the library's (major << 16) | (minor << 8) | patch; check it against
  * these macros at load time. */
 #define FA_MI355X_VERSION_MAJOR 0
@@ -229,6 +229,22 @@ int fa_fwd_v2_ex(const void* q, const void* k, const void* v, void* o,
                  void* workspace, size_t workspace_bytes,
                  const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
                  double softmax_scale, int dtype, int partial_dtype, void* stream);
+/* fa_fwd_v2_ex with flags (0, or FA_V2_COUNTERS_ZERO).  FA_V2_COUNTERS_ZERO: the caller
+ * guarantees that the workspace's completion counters are zero -- it zeroed the whole
+ * workspace once (hipMemset) and only fa_fwd_v2* calls with the same B, H, L, d,
+ * kv_tiles_per_block, blocks_per_workgroup, dtype and partial_dtype (the same counter words)
+ * have used it since, every one of which leaves its counters zero -- so the per-call counter
+ * reset, a dispatch of its own on `stream`, is skipped.  A workspace with non-zero counters under this
+ * flag gives wrong outputs or, for key blocks of >= 4096 keys, a kernel that never finishes:
+ * pass 0 when in doubt.  The reference reallocates its workspace on every call
+ * (flash_attention_v2/CUDA/flash_attention_v2.h:461-508). */
+#define FA_V2_COUNTERS_ZERO 1u
+int fa_fwd_v2_ex2(const void* q, const void* k, const void* v, void* o,
+                  int64_t B, int64_t H, int64_t L, int64_t d,
+                  int d_tile_qk, int d_tile_v, int kv_tiles_per_block, int blocks_per_workgroup,
+                  void* workspace, size_t workspace_bytes,
+                  const int64_t* q_strides, const int64_t* kv_strides, const int64_t* o_strides,
+                  double softmax_scale, int dtype, int partial_dtype, unsigned flags, void* stream);
 /* Split-KV partial forward over ONE key range (a whole KV shard, e.g. one GPU's
  * slice of the sequence).  q: [B, H, Lq, d]; k, v: [B, H, Lk, d].
  * Writes, for every query row, the normalised partial output and its log-sum-exp

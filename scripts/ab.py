@@ -59,7 +59,7 @@ def main():
         nb, ns = ctypes.c_size_t(), ctypes.c_int()
         assert libs[0].fa_fwd_v2_workspace_size_ex(B, H, L, d, args.kvtpb, args.bpw, 1, 4, ctypes.byref(nb),
                                                    ctypes.byref(ns)) == 0
-        ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
+        ws = torch.zeros(nb.value, dtype=torch.uint8, device="cuda")  # (zeroed: A/B builds without the counter reset)
         print(f"v2: kv_tiles_per_block {args.kvtpb}, {ns.value} splits, workspace {nb.value / 1e9:.2f} GB")
 
     part = None

@@ -23,6 +23,11 @@ for mode in "$@"; do
       paths=$(echo $libs | tr ',' '\n' | sed "s|^|$AB/|; s|$|.so|" | tr '\n' ' ')
       timeout -k 10 300 python scripts/ab.py --config $cfg --rounds 10 $paths > $OUT/ab_$cfg.txt 2>&1; rc=$?
       echo "ab $cfg rc=$rc"; tail -8 $OUT/ab_$cfg.txt; [ $rc -eq 0 ] || exit $rc ;;
+    abx:*)  # abx:<tag>:<lib1,lib2,...>:<ab.py arguments, '+' for spaces>
+      IFS=: read -r _ tg libs xargs <<< "$mode"
+      paths=$(echo $libs | tr ',' '\n' | sed "s|^|$AB/|; s|$|.so|" | tr '\n' ' ')
+      timeout -k 10 300 python scripts/ab.py --rounds 10 $(echo $xargs | tr '+' ' ') $paths > $OUT/ab_$tg.txt 2>&1; rc=$?
+      echo "ab $tg rc=$rc"; tail -8 $OUT/ab_$tg.txt; [ $rc -eq 0 ] || exit $rc ;;
     pmc:*)  # pmc:<lib>:<B,H,L,d>:<counters, comma separated>
       IFS=: read -r _ lib shape ctrs <<< "$mode"
       name=${lib}_$(echo $shape | tr ',' '_')_$(echo $ctrs | tr ',' '_')

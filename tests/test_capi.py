@@ -354,3 +354,15 @@ def test_d_tile_defaults():
     assert ops._d_tiles(256, None, 64) == (32, 64)
     assert ops._d_tiles(384, None, None) == (128, 128)
     assert ops._d_tiles(512, 32, None) == (32, 128)
+
+
+def test_v2_ex2_flags_validated():
+    """fa_fwd_v2_ex2 (ABI 0.4): an unknown flag bit is refused before anything is checked or
+    launched; FA_V2_COUNTERS_ZERO is the only flag."""
+    lib = L.lib()
+    st = lib.fa_fwd_v2_ex2(None, None, None, None, 1, 1, 256, 128, 32, 32, 4, 0, None, 0, None, None, None,
+                           1.0 / 128 ** 0.5, L.FA_DTYPE_BF16, L.FA_DTYPE_FP16_SCALED, 2, None)
+    assert st == L.FA_ERR_INVALID_ARG and b"flags" in lib.fa_last_error()
+    st = lib.fa_fwd_v2_ex2(None, None, None, None, 1, 1, 256, 128, 32, 32, 4, 0, None, 0, None, None, None,
+                           1.0 / 128 ** 0.5, L.FA_DTYPE_BF16, L.FA_DTYPE_FP16_SCALED, L.FA_V2_COUNTERS_ZERO, None)
+    assert st == L.FA_ERR_INVALID_ARG and b"null" in lib.fa_last_error()  # the flag itself is accepted

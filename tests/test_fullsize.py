@@ -301,3 +301,29 @@ def test_launched_kernels_reported(gpu):
         ops.combine(o_part, lse, 1, 2, torch.bfloat16)
     torch.cuda.synchronize()
     assert kl[0] == "fa_fwd16_kernel<partial> [grid 8]" and kl[1].startswith("fa_combine_kernel [grid ")
+
+
+@pytest.mark.parametrize("shape,kvt", [((1, 2, 4096), 4), ((1, 1, 16384), 4)], ids=["store-first", "arrive-first"])
+def test_v2_zeroed_workspace_skips_reset(gpu, shape, kvt):
+    """attention_v2(workspace_zeroed=True) (fa_fwd_v2_ex2, FA_V2_COUNTERS_ZERO): no counter
+    reset between calls on a workspace zeroed once -- every launch leaves its counters zero, so
+    repeated calls stay bitwise equal to the resetting path, for the store-first and the
+    arrival-first hand-offs; the launch list holds the kernel only."""
+    from exploring_flash_attention_amd import ops
+    b, h, L = shape
+    g = torch.Generator(device="cuda").manual_seed(L + 7)
+    q, k, v = (torch.randn(b, h, L, 128, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(3))
+    nbytes, _ = ops.v2_workspace_bytes(b, h, L, 128, kvt)
+    ws0 = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
+    ref = ops.attention_v2(q, k, v, kvt, workspace=ws0)
+    ws = torch.zeros(nbytes, dtype=torch.uint8, device=gpu)
+    outs = []
+    for _ in range(3):
+        with ops.launched_kernels() as kl:
+            outs.append(ops.attention_v2(q, k, v, kvt, workspace=ws, workspace_zeroed=True))
+        assert len(kl) == 1 and "in-kernel combine" in kl[0], kl
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
+    cnt = ws[-256:].view(torch.int32)  # the counters sit at the end of the workspace
+    assert int(cnt.abs().sum()) == 0
