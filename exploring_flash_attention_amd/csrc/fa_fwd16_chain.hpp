@@ -612,7 +612,12 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_chain_kernel(FwdArgs a, 
             asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
         } else if constexpr (EPI && FA_EPI_LATE) {
             // every DMA piece landed; the stores (the youngest NST operations) stay in flight
+            // (slots 8..15 issue them: final 8 store_group, one 16-byte row store each; fused 2
+            // part_store per slot plus lse_store's 2 x NQB -- the ISA check of tests/test_vmcnt.py
+            // verifies the emitted order)
             constexpr int NST = FUSED ? NF + 2 * NQB : 8;
+            static_assert(NQB * (NDB / 2) == 16 - 8, "final EPI: one row store per slot 8..15");
+            static_assert(NF == 2 * (16 - 8), "fused EPI: two partial fragments per slot 8..15");
             asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
         } else {
             __syncthreads();  // hipcc drains the DMA (vmcnt(0)) here: K(t+2), V(t+1) landed

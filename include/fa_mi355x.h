@@ -194,18 +194,28 @@ int fa_fwd_v2_workspace_size_ex(int64_t B, int64_t H, int64_t L, int64_t d,
  * ceil(CUs / query tiles) groups (about one workgroup per CU) -- for d = 128 with 16-bit inputs
  * ceil(2 * CUs / query tiles) groups (two per CU) when each group then keeps >= 4096 keys
  * (B1 H1 L16384 on 256 CUs: 4 partials per tile); d = 384 / 512: always one group;
- * a positive value fixes the group size (1: one workgroup and one HBM partial per key block, the
- * reference's layout; clamped to the number of blocks).  The plan depends only on the
- * arguments and the device's compute-unit count.  Any output pointer may be NULL. */
+ * a positive value fixes the group size (1: one key block per group, the reference's layout;
+ * clamped to the number of blocks).  *partials_per_tile counts the groups, i.e. the partials
+ * of a tile; how they are scheduled: one workgroup per group (the one-shot grid), except at
+ * d = 128 with 16-bit inputs and scaled-fp16 partials when the query tiles alone fill a grid
+ * of two workgroups per CU (B*H*ceil(L/128) >= 2 * CUs), groups of a multiple of 128 keys (at
+ * least 256) and L a multiple of 128 -- then a persistent grid of 2 workgroups per CU WALKS each query tile's
+ * groups one after another on one workgroup (the "walk", fa_last_kernels:
+ * "fa_fwd16_chain_kernel<fused walk>"), stores the first partials_per_tile - 1 partials and
+ * combines them with the last one, still in its registers.  The plan depends only on the
+ * arguments and the current device's compute-unit count.  Any output pointer may be NULL. */
 int fa_fwd_v2_split_plan(int64_t B, int64_t H, int64_t L, int64_t d, int kv_tiles_per_block,
                          int blocks_per_workgroup, int dtype, int* key_blocks,
                          int* blocks_per_wg_out, int* partials_per_tile);
 
-/* FA-v2 split-KV forward: one workgroup per (q-tile, group of key blocks, b*h) computes its
- * keys' normalised partial O and log-sum-exp into the workspace; the last workgroup of each
- * q-tile to finish combines the partials with fa_combine's formula and writes O (the
- * reduction kernel's maths without its separate pass over HBM).  One partial workgroup per
- * q-tile (fa_fwd_v2_split_plan): the plain FA-v1 kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
+/* FA-v2 split-KV forward: per (q-tile, group of key blocks, b*h) the keys' normalised partial
+ * O and log-sum-exp go into the workspace, and the tile's partials are combined with
+ * fa_combine's formula inside the same launch (the reduction kernel's maths without its
+ * separate pass over HBM) -- either by the last of the tile's workgroups to finish (one-shot
+ * grid: one workgroup per group, an arrival counter per tile), or by the workgroup that walks
+ * all of the tile's groups in turn (the persistent walk, see fa_fwd_v2_split_plan: no
+ * counters, partials_per_tile - 1 partials through HBM).  One partial per q-tile
+ * (fa_fwd_v2_split_plan): the plain FA-v1 kernel.  workspace: device buffer of at least fa_fwd_v2_workspace_size bytes,
  * 256-byte aligned, contents need not be initialised (a hipMemsetAsync of its counters
  * precedes the launch on `stream`).  d_tile_qk / d_tile_v as for fa_fwd_v1_tiled_d. */
 int fa_fwd_v2(const void* q, const void* k, const void* v, void* o,
