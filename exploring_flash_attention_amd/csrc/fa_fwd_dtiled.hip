@@ -339,303 +339,6 @@ __global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// fa_fwd_dtp_kernel -- the d-tiled forward on WAVE PAIRS (round 6; d = 384).
-//   <- flash_attention_kernel_opt (tiled-d) flash_attention_v1_tiled_d/CUDA/flash_attention_v1_opt.h:366
-//
-// Why: fa_fwd_dt_kernel's waves own 16 query rows, so every K fragment and every V^T operand it
-// reads from LDS feeds ONE 16x16x32 MFMA -- 1 KiB of LDS reads per MFMA, more than the LDS
-// serves to four SIMDs (its matrix pipe runs 40 % busy).  Here a pair of
-// waves owns 32 query rows (two 16-row query blocks, so every LDS fragment feeds two MFMAs) and
-// splits the head dim between its two waves: wave h of the pair holds the Q^T of columns
-// [h*D/2, (h+1)*D/2), accumulates its half of the QK^T contraction, and owns the O^T columns of
-// that half.  The two partial score tiles are summed through LDS (8 KiB per wave and tile, one
-// barrier the K/V stream has anyway), both waves run the (identical) online softmax on the sum
-// and each multiplies P by its half of V.  LDS bytes per MFMA: 0.64 KiB instead of 1.
-//
-// The K / V stream is fa_fwd_dt_kernel's (fa_dtiled_stream.hpp), over PAIR chunks: pair chunk
-// c of the K tile = columns [c*CQ, (c+1)*CQ) of half 0 and the same of half 1, two swizzled
-// [64 keys][CQ] images side by side in one 16 KiB slot (CQ = min(d_tile_qk, 64); V likewise
-// with CV) -- DtStream<D, 2*CQ, 2*CV, 3, 1>, the protocol tests/native/dtiled_stream_test.cpp
-// replays.  A k-step is 32 columns and the halves' k-steps run in column order, S = S_half0 +
-// S_half1 in both waves: outputs are bitwise equal across tile choices.
-// Registers (d = 384): Q^T 48, O^T 96, S 32, P 16; two workgroups per CU (80 KiB of LDS each:
-// a 3-slot ring + the 32 KiB score exchange).  d = 512 needs 64 + 128 for Q^T and O^T alone
-// and stays on fa_fwd_dt_kernel.
-#ifndef FA_DT_PAIR
-#define FA_DT_PAIR 0  // A/B: d = 384 on the wave-pair kernel
-#endif
-constexpr int kDtpSlots = 3;
-constexpr int kDtpXch = 4 * 8192;  // score exchange: 4 waves x 32 floats x 64 lanes
-int dtp_lds_bytes() { return kDtpSlots * kDtSlotB + kDtpXch; }
-
-template <typename T, int D, int CQ, int CV>
-__global__ __launch_bounds__(256, 2) void fa_fwd_dtp_kernel(FwdArgs a) {
-    using M = Mma<T>;
-    using v8 = typename M::v8;
-    static_assert(D == 384, "wave-pair d-tiled kernel: d = 384");
-    static_assert((CQ == 32 || CQ == 64) && (CV == 32 || CV == 64), "pair chunks of 32 / 64 columns per half");
-    constexpr int DH = D / 2;        // columns per wave: its contraction half and its O^T half
-    constexpr int NKSH = DH / 32;    // QK^T k-steps per half
-    constexpr int NDBH = DH / 16;    // O^T column blocks per half
-    constexpr int NKB = 4, NQB = 2, NKK = 2;
-    constexpr int ROWD = 2 * D;      // bytes per global row
-    constexpr int NSLOT = kDtpSlots;
-    constexpr float kThr = 4.f;      // defer-max threshold (log2 units), fa_fwd16_chain.hpp
-    using S = DtStream<D, 2 * CQ, 2 * CV, NSLOT, 1>;
-    constexpr int nqc = S::NQC, per_tile = S::PER_TILE;
-    constexpr int kpc = CQ / 32;     // k-steps per K half chunk
-    constexpr int bpc = CV / 16;     // O^T column blocks per V half chunk
-    constexpr int rowq = 2 * CQ, rowv = 2 * CV;   // half-chunk image row bytes
-    constexpr int HALFQ = 64 * rowq, HALFV = 64 * rowv;
-    static_assert(2 * HALFQ <= kDtSlotB && 2 * HALFV <= kDtSlotB, "a pair chunk fits a slot");
-
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* const xch = smem + NSLOT * kDtSlotB;
-
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const int qt = w % a.nqt;
-    const int64_t bh = w / a.nqt;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int h = wid & 1, pr = wid >> 1;  // column half, pair (query rows 32 pr .. 32 pr + 31)
-    const int n16 = lane & 15, g = lane >> 4;
-    const int nkv = (int)a.Lk;
-    const int ntiles = (nkv + kDtBK - 1) / kDtBK;
-    const int total = ntiles * per_tile;
-
-    // Q^T fragments of this wave's half: lane (g, n) holds Q[32 pr + 16 qb + n][h DH + 32 ks + 8 pg ..]
-    const int pg = (0x2130 >> (4 * g)) & 3;
-    const int64_t q_tile0 = (int64_t)qt * kDtRows;
-    const unsigned short* Qh = (const unsigned short*)a.q + bh * a.Lq * D + q_tile0 * D;
-    const int64_t q_rows = a.Lq - q_tile0 < kDtRows ? a.Lq - q_tile0 : kDtRows;
-    const __amdgpu_buffer_rsrc_t qrs = make_rsrc(Qh, q_rows * ROWD);
-    v8 qf[NQB][NKSH];
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-        for (int ks = 0; ks < NKSH; ++ks)
-            qf[qb][ks] = __builtin_bit_cast(
-                v8, __builtin_amdgcn_raw_buffer_load_b128(
-                        qrs, (32 * pr + 16 * qb + n16) * ROWD + (h * DH + 32 * ks) * 2 + pg * 16, 0, 0));
-
-    const char* const kbase = (const char*)a.k + bh * a.Lk * ROWD;
-    const char* const vbase = (const char*)a.v + bh * a.Lk * ROWD;
-
-    // LDS-DMA of a pair chunk: 2 halves x (C / 8) pieces of 1 KiB, wave w issuing pieces
-    // [w KPW, (w+1) KPW) -- all in one half (C / 8 pieces per half, KPW = C / 16)
-    auto src_off = [&](int piece, int rowb) {  // fa_fwd_dt_kernel's swizzled image, one half
-        const int b = piece * 1024 + lane * 16;
-        const int rg = b / (8 * rowb), rem = b % (8 * rowb);
-        const int row = 8 * rg + (rem % 512) / 64;
-        const int ch = 4 * (rem / 512) + (((rem % 64) / 16) ^ ((row >> 2) & 3));
-        return row * ROWD + ch * 16;
-    };
-    constexpr int kpw = S::KPW, vpw = S::VPW;
-    static_assert(kpw == CQ / 16 && vpw == CV / 16, "pieces per wave of a pair chunk");
-    const int khalf = (wid * kpw) / (CQ / 8), vhalf = (wid * vpw) / (CV / 8);  // the half this wave's pieces fill
-    int ksrc[kpw], vsrc[vpw];
-#pragma unroll
-    for (int p = 0; p < kpw; ++p) ksrc[p] = src_off((wid * kpw + p) % (CQ / 8), rowq);
-#pragma unroll
-    for (int p = 0; p < vpw; ++p) vsrc[p] = src_off((wid * vpw + p) % (CV / 8), rowv);
-    auto issue = [&](auto pos_c, int it, int islot) {
-        constexpr int pos = decltype(pos_c)::value;
-        constexpr bool isk = pos < nqc;
-        constexpr int c = isk ? pos : pos - nqc, dt = isk ? CQ : CV;
-        const int hf = isk ? khalf : vhalf;
-        const int valid = nkv - it * kDtBK < kDtBK ? nkv - it * kDtBK : kDtBK;
-        const __amdgpu_buffer_rsrc_t rs =
-            make_rsrc32((isk ? kbase : vbase) + (int64_t)it * kDtBK * ROWD + (hf * DH + c * dt) * 2,
-                        (valid - 1) * ROWD + 2 * dt);
-        char* const dst = smem + islot * kDtSlotB + hf * (isk ? HALFQ : HALFV);
-        constexpr int pw = isk ? kpw : vpw;
-#pragma unroll
-        for (int p = 0; p < pw; ++p)
-            dma16_asm(rs, dst + ((wid * pw + p) % (dt / 8)) * 1024, isk ? ksrc[p] : vsrc[p]);
-    };
-    int cslot = 0;
-    auto advance = [&](auto pos_c, int t) {  // fa_fwd_dt_kernel's (GRP 1)
-        constexpr int pos = decltype(pos_c)::value;
-        const int gi = t * per_tile + pos;
-        if (S::steady(gi, total))
-            wait_vm<S::after(pos)>();
-        else
-            wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (gi + S::LEAD < total)
-            issue(std::integral_constant<int, (pos + S::LEAD) % per_tile>{}, t + (pos + S::LEAD) / per_tile,
-                  S::slot_after(cslot, S::LEAD));
-        const char* const slot = smem + cslot * kDtSlotB;
-        cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
-        return slot;
-    };
-
-    // LDS read geometry (fa_fwd_dt_kernel / fa_fwd16_kernel.hpp)
-    const int rho = 8 * ((n16 >> 2) & 1) + 4 * (n16 >> 3) + (n16 & 3);
-    const unsigned kl = h * HALFQ + (rho >> 3) * (8 * rowq) + 64 * (rho & 7) + 16 * (pg ^ ((rho >> 2) & 3));
-    const int r0 = 8 * (g & 1) + 4 * (g >> 1) + (n16 >> 2);
-    const int sw = (r0 >> 2) & 3, c0 = (n16 >> 1) & 1;
-    const unsigned vrow = h * HALFV + (r0 >> 3) * (8 * rowv) + 64 * (r0 & 7) + 8 * (n16 & 1);
-    const unsigned vl_e = vrow + 16 * (c0 ^ sw), vl_o = vrow + 16 * ((2 + c0) ^ sw);
-    const int R0 = 8 * (g & 1) + 4 * (g >> 1);
-
-    f32x4 o[NDBH][NQB];
-#pragma unroll
-    for (int db = 0; db < NDBH; ++db)
-#pragma unroll
-        for (int qb = 0; qb < NQB; ++qb) o[db][qb] = f32x4{};
-    f32x4 rs[NQB] = {f32x4{}, f32x4{}};
-    float m[NQB] = {-INFINITY, -INFINITY};
-    v8 ones;
-    {
-        constexpr unsigned kOne = std::is_same_v<T, __bf16> ? 0x3F80u : 0x3C00u;
-        ones = __builtin_bit_cast(v8, u32x4{kOne | (kOne << 16), kOne | (kOne << 16), kOne | (kOne << 16),
-                                            kOne | (kOne << 16)});
-    }
-    const float c = a.scale_log2;
-
-    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-    auto vread = [](u32x2 (&vf)[4], const char* vb, int rowv_) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            vf[2 * kk] = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + kk * 32 * rowv_)));
-            vf[2 * kk + 1] = __builtin_bit_cast(
-                u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + kk * 32 * rowv_ + 16 * rowv_)));
-        }
-    };
-    // the score exchange: this wave's 32 partial scores per lane at xch + 8 KiB * wid, lane-linear
-    char* const xmine = xch + wid * 8192 + lane * 16;
-    const char* const xother = xch + (wid ^ 1) * 8192 + lane * 16;
-
-    issue(std::integral_constant<int, 0>{}, 0, 0);
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-        for (int ks = 0; ks < NKSH; ++ks) asm volatile("" : "+v"(qf[qb][ks]));
-    static_for<S::FILL - 1>([&](auto i_c) {
-        constexpr int i = decltype(i_c)::value + 1;
-        issue(std::integral_constant<int, i>{}, 0, i);
-    });
-    const char* slot = smem;
-    for (int t = 0; t < ntiles; ++t) {
-        // ---- this wave's half of S^T = K Q^T
-        f32x4 s[NKB][NQB];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) s[kb][qb] = f32x4{};
-        static_for<NKSH>([&](auto ks_c) {
-            constexpr int ks = decltype(ks_c)::value;
-            if constexpr (ks % kpc == 0) slot = advance(std::integral_constant<int, ks / kpc>{}, t);
-            u32x4 kf[NKB];
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) kf[kb] = *(const u32x4*)(slot + kl + (ks % kpc) * 512 + kb * 16 * rowq);
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb)
-                    s[kb][qb] = M::mma16(__builtin_bit_cast(v8, kf[kb]), qf[qb][ks], s[kb][qb]);
-        });
-        // ---- the two halves summed: publish mine, the first V chunk's barrier, read the partner's
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) *(f32x4*)(xmine + (kb * NQB + qb) * 1024) = s[kb][qb];
-        slot = advance(std::integral_constant<int, nqc>{}, t);
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) s[kb][qb] += *(const f32x4*)(xother + (kb * NQB + qb) * 1024);
-        if (nkv - t * kDtBK < kDtBK) {  // keys past the end (last tile only): -inf
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (t * kDtBK + 16 * kb + R0 + i >= nkv) s[kb][qb][i] = -INFINITY;
-        }
-        // ---- online softmax (base 2) of both query blocks: row max over the 4 lanes of a query
-        float mx4[NQB];
-#pragma unroll
-        for (int qb = 0; qb < NQB; ++qb) {
-            float v = fmax_nc(fmax_nc(s[0][qb][0], s[0][qb][1]), fmax_nc(s[0][qb][2], s[0][qb][3]));
-#pragma unroll
-            for (int kb = 1; kb < NKB; ++kb)
-                v = fmax_nc(v, fmax_nc(fmax_nc(s[kb][qb][0], s[kb][qb][1]), fmax_nc(s[kb][qb][2], s[kb][qb][3])));
-            mx4[qb] = v;
-        }
-        float mx[NQB];
-        quad_max2(mx4[0], mx4[1], mx[0], mx[1]);
-        mx[0] *= c;
-        mx[1] *= c;
-        if (__builtin_amdgcn_ballot_w64(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr)) {
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) {
-                const float m_new = fmaxf(m[qb], mx[qb]);
-                const float alpha = __builtin_amdgcn_exp2f(m[qb] - m_new);  // 0 on the first tile
-                m[qb] = m_new;
-                rs[qb] *= alpha;
-#pragma unroll
-                for (int db = 0; db < NDBH; ++db) o[db][qb] *= alpha;
-            }
-        }
-        u32x4 pbu[NKK][NQB];  // P^T fragments (k-order as fa_fwd16_kernel.hpp)
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int kb = 2 * kk + (j >> 1), i = 2 * (j & 1);
-                    pbu[kk][qb][j] = pack2<T>(__builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][qb][i], c, -m[qb])),
-                                              __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][qb][i + 1], c, -m[qb])));
-                }
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk)
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) rs[qb] = M::mma16(ones, __builtin_bit_cast(v8, pbu[kk][qb]), rs[qb]);
-
-        // ---- this wave's O^T half += V^T P^T over the V pair chunks
-        static_for<NDBH>([&](auto db_c) {
-            constexpr int db = decltype(db_c)::value;
-            if constexpr (db % bpc == 0 && db > 0) slot = advance(std::integral_constant<int, nqc + db / bpc>{}, t);
-            u32x2 vf[4];
-            vread(vf, slot + ((db & 1) ? vl_o : vl_e) + 512 * ((db % bpc) >> 1), rowv);
-#pragma unroll
-            for (int kk = 0; kk < NKK; ++kk) {
-                const u32x4 vv = {vf[2 * kk][0], vf[2 * kk][1], vf[2 * kk + 1][0], vf[2 * kk + 1][1]};
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb)
-                    o[db][qb] = M::mma16(__builtin_bit_cast(v8, vv), __builtin_bit_cast(v8, pbu[kk][qb]), o[db][qb]);
-            }
-        });
-    }
-
-    // ---- epilogue: lane (g, n) holds O^T[h DH + 16 db + 4 g + i][query 32 pr + 16 qb + n]; dv
-    // blocks 2e and 2e+1 paired by v_permlane16_swap into one 16-byte store per lane
-#pragma unroll
-    for (int qb = 0; qb < NQB; ++qb) {
-        const int64_t q_row = q_tile0 + 32 * pr + 16 * qb + n16;
-        if (q_row >= a.Lq) continue;
-        const float inv = 1.f / rs[qb][0];
-        unsigned short* const Oh = (unsigned short*)a.o + (bh * a.Lq + q_row) * D + h * DH;
-#pragma unroll
-        for (int e = 0; e < NDBH / 2; ++e) {
-            const unsigned x0 = pack2<T>(o[2 * e][qb][0] * inv, o[2 * e][qb][1] * inv);
-            const unsigned x1 = pack2<T>(o[2 * e][qb][2] * inv, o[2 * e][qb][3] * inv);
-            const unsigned y0 = pack2<T>(o[2 * e + 1][qb][0] * inv, o[2 * e + 1][qb][1] * inv);
-            const unsigned y1 = pack2<T>(o[2 * e + 1][qb][2] * inv, o[2 * e + 1][qb][3] * inv);
-            const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-            const u32x4 u = {s0[0], s1[0], s0[1], s1[1]};
-            *(u32x4*)(Oh + 32 * e + 16 * (g & 1) + 8 * (g >> 1)) = u;
-        }
-    }
-}
-
 // the kernel geometry the C ABI reports for a wide head dim (fa_kernel_geometry)
 void dtiled_geometry(Elem, int d, int* rows, int* threads, int* lds) {
     *rows = kDtRows;
@@ -667,28 +370,9 @@ static hipError_t launch_dt(const FwdArgs& a, const dim3& grid, int lds, hipStre
     return hipErrorInvalidValue;
 }
 
-// d = 384 on the wave-pair kernel: pair chunks of min(d_tile, 64) columns per half
-template <typename T>
-static hipError_t launch_dtp(const FwdArgs& a, const dim3& grid, hipStream_t s) {
-    auto go = [&](auto kern) {
-        note_kernel("fa_fwd_dtp_kernel", grid.x);
-        hipLaunchKernelGGL(kern, grid, dim3(256), dtp_lds_bytes(), s, a);
-        return hipGetLastError();
-    };
-    const bool q64 = a.d_tile_qk >= 64, v64 = a.d_tile_v >= 64;
-    if (q64 && v64) return go(fa_fwd_dtp_kernel<T, 384, 64, 64>);
-    if (q64) return go(fa_fwd_dtp_kernel<T, 384, 64, 32>);
-    if (v64) return go(fa_fwd_dtp_kernel<T, 384, 32, 64>);
-    return go(fa_fwd_dtp_kernel<T, 384, 32, 32>);
-}
-
 hipError_t launch_fwd_dtiled(Elem t, int d, const FwdArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((int64_t)a.nqt * a.BH));
     const int lds = dtiled_lds_bytes(d);
-    if (FA_DT_PAIR && d == 384) {
-        if (t == Elem::BF16) return launch_dtp<__bf16>(a, grid, s);
-        if (t == Elem::F16) return launch_dtp<_Float16>(a, grid, s);
-    }
     if (t == Elem::BF16) {
         if (d == 384) return launch_dt<__bf16, 384>(a, grid, lds, s);
         if (d == 512) return launch_dt<__bf16, 512>(a, grid, lds, s);
