@@ -28,6 +28,10 @@ for mode in "$@"; do
       paths=$(echo $libs | tr ',' '\n' | sed "s|^|$AB/|; s|$|.so|" | tr '\n' ' ')
       timeout -k 10 300 python scripts/ab.py --rounds 10 $(echo $xargs | tr '+' ' ') $paths > $OUT/ab_$tg.txt 2>&1; rc=$?
       echo "ab $tg rc=$rc"; tail -8 $OUT/ab_$tg.txt; [ $rc -eq 0 ] || exit $rc ;;
+    cmp:*)  # cmp:<libA>:<libB>:<d>  (scripts/cmp_libs.py)
+      IFS=: read -r _ la lb dd <<< "$mode"
+      timeout -k 10 300 python scripts/cmp_libs.py $AB/$la.so $AB/$lb.so $dd > $OUT/cmp_${la}_${lb}.txt 2>&1; rc=$?
+      echo "cmp $la $lb rc=$rc"; tail -4 $OUT/cmp_${la}_${lb}.txt; [ $rc -eq 0 ] || exit $rc ;;
     pmc:*)  # pmc:<lib>:<B,H,L,d>:<counters, comma separated>
       IFS=: read -r _ lib shape ctrs <<< "$mode"
       name=${lib}_$(echo $shape | tr ',' '_')_$(echo $ctrs | tr ',' '_')
