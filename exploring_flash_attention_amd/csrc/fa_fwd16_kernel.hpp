@@ -536,6 +536,12 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             return __builtin_amdgcn_readfirstlane(*last_flag);
         };
         int last = af ? arrive() : 0;
+#if FA_STAMPS
+        // (diagnostic builds: 10 the hand-off verdict, 11 the combine's start, 12 = 1 for the
+        // tile's last workgroup; 4 / 5 / 9 as in kFinal, for the last one after its O)
+        if (af) FA_STAMP(10);
+        FA_STAMP_V(12, last);
+#endif
         // this block's partial as stored: 16-bit pairs (or fp32) per fragment, lse of the row
         using Frag = std::conditional_t<sizeof(PT) == 4, f32x4, u32x2>;
         Frag mine[NQB][NDB];
@@ -578,9 +584,23 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             __syncthreads();
             if (af) {
                 if (tid == 0) __hip_atomic_fetch_add(a.counters + grp, 0x10000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if FA_STAMPS
+                FA_STAMP(4);
+                FA_STAMP(5);
+                FA_STAMP_V(9, __builtin_amdgcn_s_memrealtime());
+#endif
                 return;
             }
             last = arrive();
+#if FA_STAMPS
+            FA_STAMP(10);
+            FA_STAMP_V(12, last);
+            if (!last) {
+                FA_STAMP(4);
+                FA_STAMP(5);
+                FA_STAMP_V(9, __builtin_amdgcn_s_memrealtime());
+            }
+#endif
             if (!last) return;
         }
         if (tid == 0) {
@@ -598,6 +618,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             a.counters[grp] = 0;  // leave the counter zero for the next launch
         }
         __syncthreads();
+        FA_STAMP(11);
 
         // Sum in split order 0, 1, ... whatever workgroup came last, so that O is bitwise
         // repeatable.
@@ -630,26 +651,27 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
         constexpr int U = sizeof(PT) == 4 ? 2 : 4;
         auto clampsp = [&](int sp) { return sp < ns ? sp : ns - 1; };
         // (at most U blocks -- the library's splits at d = 128 -- everything is loaded in one
-        // batch: one memory round trip on the tile's critical path instead of two)
+        // batch per query block.  Both query blocks in one batch (128 more VGPRs) spilled the
+        // loaded partials and ran B1 H2 L4096 27.7 -> 31.4 us: profiles/r06/ab_*_combine_batch2)
+        auto load_batch = [&](int qb, int sp0, float (&lv)[U], float (&ev)[U], Frag (&pv)[U][NDB]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int sp = clampsp(sp0 + u);
+                lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1));
+                if constexpr (SCALED)
+                    ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) pv[u][db] = load_frag(sp, db * NQB + qb);
+                if (sp == split) {
+                    lv[u] = lse_mine[qb];
+                    ev[u] = esc[qb];
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db) pv[u][db] = mine[qb][db];
+                }
+            }
+        };
 #pragma unroll
         for (int qb = 0; qb < NQB; ++qb) {
-            auto load_batch = [&](int sp0, float (&lv)[U], float (&ev)[U], Frag (&pv)[U][NDB]) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sp = clampsp(sp0 + u);
-                    lv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(l_rsrc(sp), lse_off(qb), 0, SC1));
-                    if constexpr (SCALED)
-                        ev[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e_rsrc(sp), lse_off(qb), 0, SC1));
-#pragma unroll
-                    for (int db = 0; db < NDB; ++db) pv[u][db] = load_frag(sp, db * NQB + qb);
-                    if (sp == split) {
-                        lv[u] = lse_mine[qb];
-                        ev[u] = esc[qb];
-#pragma unroll
-                        for (int db = 0; db < NDB; ++db) pv[u][db] = mine[qb][db];
-                    }
-                }
-            };
             float Mx = -INFINITY, E = -1000.f;
             f32x4 acc[NDB];
 #pragma unroll
@@ -669,7 +691,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             if (ns <= U) {
                 float lv[U], ev[U];
                 Frag pv[U][NDB];
-                load_batch(0, lv, ev, pv);
+                load_batch(qb, 0, lv, ev, pv);
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     Mx = fmaxf(Mx, lv[u]);
@@ -699,7 +721,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                 for (int sp0 = 0; sp0 < ns; sp0 += U) {
                     float lv[U], ev[U];
                     Frag pv[U][NDB];
-                    load_batch(sp0, lv, ev, pv);
+                    load_batch(qb, sp0, lv, ev, pv);
                     accumulate(sp0, lv, ev, pv);
                 }
             }
@@ -714,6 +736,12 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
             if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o_final + o_head + q_row * orow, acc, inv_w);
         }
+#if FA_STAMPS
+        FA_STAMP(4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FA_STAMP(5);
+        FA_STAMP_V(9, __builtin_amdgcn_s_memrealtime());
+#endif
     }
 }
 

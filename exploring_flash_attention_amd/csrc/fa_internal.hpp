@@ -29,6 +29,8 @@ constexpr int kRowsum16Mask = 0x7;
 constexpr bool rs16_on(int d, int mode, bool tail, bool strided) {
     return (kRowsum16Mask & d_bit(d)) != 0 && (d > 32 || (mode == 0 && !tail && !strided));
 }
+// (d = 32 at three waves per SIMD: 147 VGPRs, no scratch, C2 49.8 -> 50.4 us -- the 60 B of
+// scratch at four are spilled around the last KV step only; profiles/r06/ab_c2_wps3_noscratch.txt)
 constexpr int kernel_wps(int d, int mode, bool tail, bool strided) {
     return rs16_on(d, mode, tail, strided) && d <= 32 ? 4
            : rs16_on(d, mode, tail, strided) && d == 64 ? 3

@@ -1,6 +1,6 @@
 """Summarise the PMC passes of scripts/profile_pmc.sh into per-launch HBM traffic.
 
-    python scripts/traffic.py gpurun_out/pmc_c3 c3 [out.json]
+    python scripts/traffic.py gpurun_out/pmc_c3 c3 [out.json [source label]]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts exactly half
 the bytes of a wide (16 B/lane) coalesced read stream -- every read of the forward kernel
@@ -40,7 +40,18 @@ def main():
         old = {}
         if os.path.exists(out):
             old = json.load(open(out))
-        old.update(res)
+        prev = old.get(cfg, {})
+        # keep the entry's labels (kernel, algorithmic bytes), record where the new counters
+        # came from and what the entry said before
+        for key in ("kernel", "algorithmic_bytes"):
+            if key in prev:
+                rec[key] = prev[key]
+        if "algorithmic_bytes" in rec and "bytes_per_launch" in rec:
+            rec["ratio_to_algorithmic"] = round(rec["bytes_per_launch"] / rec["algorithmic_bytes"], 3)
+        rec["source"] = sys.argv[4] if len(sys.argv) > 4 else d
+        if "bytes_per_launch" in prev:
+            rec["previous"] = {k: prev[k] for k in ("bytes_per_launch", "kernel", "source") if k in prev}
+        old[cfg] = rec
         json.dump(old, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
