@@ -210,7 +210,7 @@ def _d_tiles(d, d_tile_qk, d_tile_v):
     128 above, where the d-tiled kernel streams K / V in tile-wide column chunks.  The output
     is bitwise the same for every tile choice, only the speed differs: d = 512 B32 H8 L1024,
     32/32 0.931 ms against 128/128 0.682 ms (24 chunk waits + barriers per 64-key tile against
-    6; gpurun_out/r05i/dtile_sweep.txt, profiles/r05/dtile_sweep.txt)."""
+    6; scripts/dtile_sweep.py, profiles/r05/dtile_sweep.txt)."""
     dflt = min(32, d) if d <= 256 else 128
     return (dflt if d_tile_qk is None else int(d_tile_qk),
             dflt if d_tile_v is None else int(d_tile_v))

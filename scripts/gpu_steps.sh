@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-6 GPU steps, one mode per call (each GPU step under its own time limit, chained so that
+# GPU steps for one gpurun call, one mode per argument (each GPU step under its own time limit, chained so that
 # the first failure ends the call).  Output under gpurun_out/<tag>/.
-#   bash scripts/gpu_r06.sh <tag> tests|bench|ab|pmc ...
+#   bash scripts/gpu_steps.sh <tag> tests|bench|ab|pmc ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
