@@ -9,9 +9,6 @@
 #ifndef FA_CHAIN
 #define FA_CHAIN 1  // d = 128 final mode: the chained persistent grid (fa_fwd16_chain.hpp)
 #endif
-#ifndef FA_KS2
-#define FA_KS2 0  // A/B: fused split-KV at <= 1 workgroup per CU as two key halves per workgroup
-#endif
 
 
 namespace fa {
@@ -41,23 +38,6 @@ static hipError_t launch_one(const FwdArgs& a, hipStream_t s) {
                 return hipGetLastError();
             }
         }
-#if FA_KS2
-        if constexpr (MODE == kFused) {
-            // at most one workgroup per CU (a 4-wave workgroup would run one wave per SIMD): two
-            // key halves per 8-wave workgroup, merged on chip (fa_fwd16_kernel.hpp, KS2); every
-            // split whole and an even number >= 4 of 64-key tiles
-            if (nblk <= device_cus(s) && a.kv_per_split % 256 == 0 && a.Lk % a.kv_per_split == 0 &&
-                a.Lq % kBQ == 0) {
-                static const hipError_t attr = hipFuncSetAttribute(
-                    (const void*)fa_fwd16_ks2_kernel<T, PT, D, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * lds);
-                if (attr != hipSuccess) return attr;
-                note_kernel("fa_fwd16_ks2_kernel<fused split, two key halves per workgroup>", nblk);
-                hipLaunchKernelGGL((fa_fwd16_ks2_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(2 * kThreads),
-                                   2 * lds, s, a);
-                return hipGetLastError();
-            }
-        }
-#endif
         if (a.Lk % bk_for(D) == 0 && a.kv_per_split % bk_for(D) == 0) {  // no key tail in any split
             note_kernel(kernel_label(true, MODE, false), nblk);
             hipLaunchKernelGGL((fa_fwd16_kernel<T, PT, D, MODE>), dim3((unsigned)nblk), dim3(kThreads), lds, s, a);

@@ -32,13 +32,6 @@
 #pragma once
 #include "fa_device.hpp"
 
-#ifndef FA_KS2_G1EXIT
-#define FA_KS2_G1EXIT 0
-#endif
-#ifndef FA_KS2_G1LATE
-#define FA_KS2_G1LATE 0
-#endif
-
 namespace fa {
 
 template <typename X> struct TypeTag { using type = X; };
@@ -61,18 +54,8 @@ struct NoHook {
 // One work item (query tile, split, b*h) of the kernel; `at_loop_end` runs once, right after
 // the KV loop's last barrier (round 4's dynamic-claim experiment claimed its next item there;
 // measured and removed).
-// KS2 (fused mode, fa_fwd16_ks2_kernel): an 8-wave workgroup whose two 4-wave groups take the
-// two halves of the split's keys for the same 128 query rows, each with its own K / V ring --
-// for grids of at most one workgroup per CU, where a 4-wave workgroup runs one wave per SIMD.
-// Group 1 runs half a step behind group 0 (one extra barrier before its prologue, a barrier
-// between phase A and phase B of every step), so that each SIMD pairs one wave's QK^T and
-// exponentials with the other's P.V, as two free-running workgroups pair.  After the loop
-// group 1 hands its O, row maxima and row sums to group 0 through LDS and group 0 merges them
-// (the split-KV combine's formula); group 1 then runs the same epilogue code with every memory
-// operation disabled, so that both groups pass the same barriers.
-template <typename T, typename PT, int D, int MODE, bool STR = false, typename Hook = NoHook, bool KS2 = false>
+template <typename T, typename PT, int D, int MODE, bool STR = false, typename Hook = NoHook>
 __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, const Hook& at_loop_end = Hook{}) {
-    static_assert(!KS2 || (MODE == kFused && !STR), "two key halves per workgroup: fused contiguous launches");
     using M = Mma<T>;
     using v8 = typename M::v8;
     static_assert(D == 128, "16x16x32 kernel: d = 128");
@@ -93,36 +76,23 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
     static_assert(EXPA >= 19 && EXPA <= 32, "key step 0 packs (phase A slots 6..13) follow their exponentials");
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane((tid >> 6) & (kWaves - 1));
-    const int kh = KS2 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;  // key half (KS2)
-    const bool act = kh == 0;  // (KS2: group 1's epilogue memory operations are disabled)
-#if FA_KS2_G1LATE
-    if (KS2 && kh == 1) asm volatile("s_barrier" ::: "memory");  // group 1: half a step behind
-#endif
-    char* const kring = smem + kh * 4 * TILEB;  // K ring: 2 slots
-    char* const vring = kring + 2 * TILEB;       // V ring: 2 slots
+    char* const kring = smem;              // K ring: 2 slots
+    char* const vring = smem + 2 * TILEB;  // V ring: 2 slots
 
     int qt, split;
     int64_t bh;
     decode_item(a, w, qt, split, bh);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n16 = lane & 15, g = lane >> 4;
     // (FA_STAMPS diagnostic builds only, fa_fwd_kernel.hpp; slots as scripts/stamps.py reads them)
     FA_STAMP_V(8, __builtin_amdgcn_s_memrealtime());
     FA_STAMP(0);
     FA_STAMP_V(6, __builtin_amdgcn_s_getreg(4 | (31 << 11)));
     FA_STAMP_V(7, __builtin_amdgcn_s_getreg(20 | (31 << 11)));
-    int64_t kv_begin = (int64_t)split * a.kv_per_split;
-    int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
-    if constexpr (KS2) {  // (the launcher: every split an even number of tiles, so both halves
-                          // run the same steps and pass the same barriers)
-        const int64_t half = (kv_end - kv_begin) / 2;
-        if (kh == 0)
-            kv_end = kv_begin + half;
-        else
-            kv_begin += half;
-    }
+    const int64_t kv_begin = (int64_t)split * a.kv_per_split;
+    const int64_t kv_end = kv_begin + a.kv_per_split < a.Lk ? kv_begin + a.kv_per_split : a.Lk;
     const int ntiles = (int)((kv_end - kv_begin) / kBK);
 
     const int64_t q_tile0 = (int64_t)qt * kBQ;
@@ -351,7 +321,6 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
 
         // ---- phase B: P.V(t) || exponentials of t (rest), row max of t+1
         __builtin_amdgcn_s_setprio(0);
-        if constexpr (KS2) asm volatile("s_barrier" ::: "memory");  // the half-step offset (above)
         // slot J: key step kk = J / 9; J % 9 < 8: P.V of column block J % 9, J % 9 == 8: row sums
         u32x2 vf[VA + 1][2];
         float m4[4];
@@ -397,9 +366,6 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
     dma_tile(kbase, kring, 0);
     dma_tile(vbase, vring, 0);
     if (ntiles > 1) dma_tile(kbase, kring + TILEB, 1);
-#if !FA_KS2_G1LATE
-    if (KS2 && kh == 1) asm volatile("s_barrier" ::: "memory");  // group 1: half a step behind
-#endif
 #pragma unroll
     for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
@@ -444,48 +410,6 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
 
     FA_STAMP(3);
     at_loop_end();
-    if constexpr (KS2) {
-        // group 0 passes the barrier that closes group 1's last step; group 1 writes its O into
-        // its own ring (every wave of it finished reading there), its {m, l} pairs behind the
-        // LDS flag word of group 0's ring (group 0's loop ended); group 0 merges
-        constexpr int NF = NDB * NQB;
-        if (kh == 0) asm volatile("s_barrier" ::: "memory");
-        f32x4* const xo = (f32x4*)(smem + 4 * TILEB) + wid * NF * 64 + lane;
-        f32x4* const xm = (f32x4*)(smem + 1024) + wid * 64 + lane;
-        if (kh == 1) {
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                for (int qb = 0; qb < NQB; ++qb) xo[(db * NQB + qb) * 64] = o[db][qb];
-            *xm = f32x4{m[0], m[1], rs[0][0], rs[1][0]};
-        }
-        __syncthreads();
-        if (kh == 0) {
-            const f32x4 ml = *xm;
-#pragma unroll
-            for (int qb = 0; qb < NQB; ++qb) {
-                const float mn = fmaxf(m[qb], ml[qb]);
-                const float a0 = __builtin_amdgcn_exp2f(m[qb] - mn), a1 = __builtin_amdgcn_exp2f(ml[qb] - mn);
-                m[qb] = mn;
-                const float l = rs[qb][0] * a0 + ml[2 + qb] * a1;
-                rs[qb] = f32x4{l, l, l, l};
-#pragma unroll
-                for (int db = 0; db < NDB; ++db) o[db][qb] = o[db][qb] * a0 + xo[(db * NQB + qb) * 64] * a1;
-            }
-        }
-#if FA_KS2_G1EXIT
-        if (kh == 1) {
-            // group 1 passes the fused epilogue's barriers only (group 0's partial stores drained,
-            // its arrival verdict, the combine's start), as many as group 0's path through it
-            const bool af = a.arrive_first != 0;
-            if (!af) __syncthreads();
-            __syncthreads();
-            const int last = __builtin_amdgcn_readfirstlane(*(const int*)smem);
-            if (af || last) __syncthreads();
-            return;
-        }
-#endif
-    }
     // ---- epilogue: lane (g, n) holds O^T[16*db + 4*g + i][query 16*qb + n].  A 16-bit row is
     // stored 16 bytes per lane: dv blocks 2e and 2e+1 are paired by one v_permlane16_swap per
     // dword, lane group g then holds columns 32*e + 16*(g&1) + 8*(g>>1) .. +7.
@@ -595,10 +519,10 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
         auto blk_of = [&](int sp) { return (int64_t)sp * a.BH * a.nqt + grp; };
         // (the own block's ranges are empty in the combine: its loads return 0 and move no bytes)
         auto o_rsrc = [&](int sp) {
-            return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, sp == split || !act ? 0 : (int64_t)BLK * sizeof(PT));
+            return make_rsrc((const PT*)a.o + blk_of(sp) * BLK, sp == split ? 0 : (int64_t)BLK * sizeof(PT));
         };
-        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, sp == split || !act ? 0 : (int64_t)kBQ * 4); };
-        auto e_rsrc = [&](int sp) { return make_rsrc(a.esc + blk_of(sp) * kBQ, sp == split || !act ? 0 : (int64_t)kBQ * 4); };
+        auto l_rsrc = [&](int sp) { return make_rsrc(a.lse + blk_of(sp) * kBQ, sp == split ? 0 : (int64_t)kBQ * 4); };
+        auto e_rsrc = [&](int sp) { return make_rsrc(a.esc + blk_of(sp) * kBQ, sp == split ? 0 : (int64_t)kBQ * 4); };
         auto frag_off = [&](int f) { return (((wid * NF + f) * 64 + lane) * 4) * (int)sizeof(PT); };
         auto lse_off = [&](int qb) { return (wid * 32 + 16 * qb + n16) * 4; };
         int* const last_flag = (int*)smem;  // LDS is free: the KV loop ended with a barrier
@@ -637,9 +561,9 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
             lse_mine[qb] = __int_as_float(__builtin_amdgcn_ds_bpermute(n16 * 4, __float_as_int(lse)));
         }
         if (!last) {
-            const __amdgpu_buffer_rsrc_t ors = make_rsrc((const PT*)a.o + blk_of(split) * BLK, act ? (int64_t)BLK * sizeof(PT) : 0);
-            const __amdgpu_buffer_rsrc_t lrs = make_rsrc(a.lse + blk_of(split) * kBQ, act ? (int64_t)kBQ * 4 : 0);
-            const __amdgpu_buffer_rsrc_t ers = make_rsrc(a.esc + blk_of(split) * kBQ, act ? (int64_t)kBQ * 4 : 0);
+            const __amdgpu_buffer_rsrc_t ors = make_rsrc((const PT*)a.o + blk_of(split) * BLK, (int64_t)BLK * sizeof(PT));
+            const __amdgpu_buffer_rsrc_t lrs = make_rsrc(a.lse + blk_of(split) * kBQ, (int64_t)kBQ * 4);
+            const __amdgpu_buffer_rsrc_t ers = make_rsrc(a.esc + blk_of(split) * kBQ, (int64_t)kBQ * 4);
 #pragma unroll
             for (int qb = 0; qb < NQB; ++qb) {
 #pragma unroll
@@ -810,7 +734,7 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
                 inv_w = 1.f;
             }
             const int64_t q_row = q_tile0 + wid * 32 + 16 * qb + n16;
-            if (act && q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o_final + o_head + q_row * orow, acc, inv_w);
+            if (q_row < a.Lq) store_row16(TypeTag<T>{}, (unsigned short*)a.o_final + o_head + q_row * orow, acc, inv_w);
         }
 #if FA_STAMPS
         FA_STAMP(4);
@@ -824,12 +748,6 @@ __device__ __forceinline__ void fa_fwd16_item(const FwdArgs& a, const int w, con
 template <typename T, typename PT, int D, int MODE, bool STR = false>
 __global__ __launch_bounds__(kThreads, 2) void fa_fwd16_kernel(FwdArgs a) {
     fa_fwd16_item<T, PT, D, MODE, STR>(a, xcd_remap(blockIdx.x, gridDim.x));
-}
-
-// fused split-KV, two key halves per 8-wave workgroup (KS2 above); one workgroup per CU
-template <typename T, typename PT, int D, int MODE>
-__global__ __launch_bounds__(2 * kThreads, 1) void fa_fwd16_ks2_kernel(FwdArgs a) {
-    fa_fwd16_item<T, PT, D, MODE, false, NoHook, true>(a, xcd_remap(blockIdx.x, gridDim.x));
 }
 
 }  // namespace fa
