@@ -13,11 +13,10 @@
 
 namespace fa {
 
-template <int D, int DQ, int DV, int NSLOT, int GRP_REQ, int W = 4>
+template <int D, int DQ, int DV, int NSLOT, int GRP_REQ>
 struct DtStream {
     static constexpr int NQC = D / DQ, NVC = D / DV, PER_TILE = NQC + NVC;
-    static constexpr int KPW = DQ * 4 / (32 * W), VPW = DV * 4 / (32 * W);  // pieces per wave (W waves)
-    static_assert(KPW >= 1 && VPW >= 1 && KPW * W * 8 == DQ && VPW * W * 8 == DV, "whole pieces per wave");
+    static constexpr int KPW = DQ / 32, VPW = DV / 32;
     static constexpr int GRP = (GRP_REQ == 2 && PER_TILE % 2 == 0 && NSLOT == 4) ? 2 : 1;
     static constexpr int LEAD = GRP == 2 ? 2 : NSLOT - 1;  // chunks between a consumer and the issue
     static constexpr int FILL = GRP == 2 ? 2 : NSLOT - 1;  // chunks issued before the loop

@@ -33,19 +33,9 @@
 #include "fa_device.hpp"
 #include "fa_dtiled_stream.hpp"
 
-#ifndef FA_DT_PROBE
-#define FA_DT_PROBE 0
-#endif
-#ifndef FA_DT_W8
-#define FA_DT_W8 0  // A/B: one 8-wave workgroup per CU (128 rows) sharing one chunk ring
-#endif
-#ifndef FA_DT_W8_SLOTS
-#define FA_DT_W8_SLOTS 4
-#endif
-
 namespace fa {
 
-constexpr int kDtWaves = FA_DT_W8 ? 8 : 4;
+constexpr int kDtWaves = 4;
 constexpr int kDtRows = 16 * kDtWaves;  // query rows per workgroup
 constexpr int kDtBK = 64;               // keys per tile
 constexpr int kDtMaxChunk = 128;        // columns per LDS chunk at most
@@ -66,7 +56,6 @@ constexpr int dt_wps(int d) { return d <= 384 ? FA_DT384_WPS : FA_DT512_WPS; }
 #define FA_DT_SLOTS2 0  // 0: the measured choice above; n: n slots at both head dims (A/B builds)
 #endif
 constexpr int dt_slots(int d) {
-    if (FA_DT_W8) return FA_DT_W8_SLOTS;
     return dt_wps(d) == 2 ? (FA_DT_SLOTS2 > 0 ? FA_DT_SLOTS2 : d <= 384 ? 3 : 4) : 8;
 }
 
@@ -96,7 +85,7 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t rs, const char*
 #pragma clang diagnostic pop
 
 template <typename T, int D, int DQ, int DV>
-__global__ __launch_bounds__(kDtWaves * 64, FA_DT_W8 ? 1 : dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
+__global__ __launch_bounds__(256, dt_wps(D)) void fa_fwd_dt_kernel(FwdArgs a) {
     using M = Mma<T>;
     using v8 = typename M::v8;
     static_assert(D % 128 == 0 && D > 256 && D <= 512, "d-tiled kernel: d = 384 or 512");
@@ -123,7 +112,7 @@ __global__ __launch_bounds__(kDtWaves * 64, FA_DT_W8 ? 1 : dt_wps(D)) void fa_fw
 #ifndef FA_DT_GROUP
 #define FA_DT_GROUP 1  // 2: chunks made readable in pairs, one barrier per pair (4 slots)
 #endif
-    using S = DtStream<D, DQ, DV, NSLOT, FA_DT_GROUP, kDtWaves>;
+    using S = DtStream<D, DQ, DV, NSLOT, FA_DT_GROUP>;
     constexpr int nqc = S::NQC, per_tile = S::PER_TILE;
     constexpr int kpc = DQ / 32;          // QK^T k-steps per K chunk
     constexpr int bpc = DV / 16;          // O^T column blocks per V chunk
@@ -191,19 +180,13 @@ __global__ __launch_bounds__(kDtWaves * 64, FA_DT_W8 ? 1 : dt_wps(D)) void fa_fw
                 wait_vm<0>();
             // the barrier as inline asm with a memory clobber: no memory operation (the next DMA
             // into a retired slot above all) may be moved across it, and no drain is implied
-#if FA_DT_PROBE & 1
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
-#if !(FA_DT_PROBE & 2)
             static_for<S::GRP>([&](auto j_c) {
                 constexpr int j = decltype(j_c)::value, np = pos + S::LEAD + j;
                 if (gi + S::LEAD + j < total)
                     issue(std::integral_constant<int, np % per_tile>{}, t + np / per_tile,
                           S::slot_after(cslot, S::LEAD + j));
             });
-#endif
         }
         const char* const slot = smem + cslot * kDtSlotB;
         cslot = cslot == NSLOT - 1 ? 0 : cslot + 1;
@@ -373,14 +356,14 @@ static hipError_t launch_dt(const FwdArgs& a, const dim3& grid, int lds, hipStre
     auto pick_v = [&](auto dq_c) -> hipError_t {
         constexpr int DQ = decltype(dq_c)::value;
         switch (a.d_tile_v) {
-            case 32: return go(fa_fwd_dt_kernel<T, D, DQ, FA_DT_W8 ? 64 : 32>);
+            case 32: return go(fa_fwd_dt_kernel<T, D, DQ, 32>);
             case 64: return go(fa_fwd_dt_kernel<T, D, DQ, 64>);
             case 128: return go(fa_fwd_dt_kernel<T, D, DQ, 128>);
         }
         return hipErrorInvalidValue;
     };
     switch (a.d_tile_qk) {
-        case 32: return pick_v(std::integral_constant<int, FA_DT_W8 ? 64 : 32>{});
+        case 32: return pick_v(std::integral_constant<int, 32>{});
         case 64: return pick_v(std::integral_constant<int, 64>{});
         case 128: return pick_v(std::integral_constant<int, 128>{});
     }
