@@ -600,7 +600,8 @@ int fa_fwd_v2_ex2(const void* q, const void* k, const void* v, void* o, int64_t 
     // memory round trip on the tile's critical path when its workgroups finish together, so
     // only for key blocks of >= 4096 keys.  Round 5, d = 128 bf16 (profiles/r05/ab,
     // profiles/r05/hbm_traffic_r05.json): B1 H1 L16384 (4 blocks of 4096) 127.5 -> 127.2 us and
-    // 72.7 -> 64.1 MB per launch; B1 H2 L4096 (4 of 1024) 28.7 -> 31.0 us.
+    // 72.7 -> 64.1 MB per launch; B1 H2 L4096 (4 of 1024) 28.7 -> 31.0 us (round 6 again:
+    // 27.4 -> 30.0 us, B1 H4 L4096 with 2 of 2048 42.1 -> 43.1 us; profiles/r06/ab_b1h*_af.txt).
     a.arrive_first = a.kv_per_split >= 4096;
     a.counters = (unsigned*)((char*)workspace + w.cnt_off);
     a.o_final = o;
