@@ -15,7 +15,10 @@ Measured inputs (profiles/r05/seam/stamps_c3_chain*.txt)
 Dynamic variants: the last items cut into `parts` key ranges claimed from one global queue,
 each costing 16/parts steps + the seam + `split` steps (partial store + combine of a split
 tile) + `claim` steps (a returning device-scope atomic under load: ~6k cycles = ~2 steps,
-round 2's measurement).
+round 2's measurement).  The split cost measured in round 6 (scripts/split_stamps.py,
+profiles/r06/split_stamps_*.txt): loop end -> hand-off verdict 1.1-2.4 us, the combine of 2
+partials + O 2.7 + 0.4 us -> ~2.6 steps of 1.7 us on the last piece of a tile (the `measured`
+rows); 0.5 is a lower bound.
 """
 import os
 import statistics
@@ -79,7 +82,7 @@ def main():
     rows = [("static lists (shipped)", dict())]
     for k in (3, 2):
         for parts in (2, 4):
-            for split, claim in ((0.0, 0.0), (0.5, 0.0), (0.5, 2.0)):
+            for split, claim in ((0.0, 0.0), (0.5, 0.0), (0.5, 2.0), (2.6, 0.0), (2.6, 2.0)):
                 rows.append((f"{k} static + {4 - k} items as {parts} key ranges, split {split}, claim {claim}",
                              dict(static_items=k, parts=parts, split=split, claim=claim)))
     out = ["C3 chained grid, modelled loop ends (us): max (= the kernel's end) / median / min",
