@@ -56,7 +56,7 @@ def test_version_and_geometry():
         L.geometry(96)
     # the d-tiled kernels: 64 query rows, 64-key tiles, a ring of 16 KiB chunk images (8 slots
     # at d = 512: one workgroup per CU; 4 at d = 384: two)
-    assert L.geometry(512) == (64, 64, 256, 4 * 16384) and L.geometry(384) == (64, 64, 256, 3 * 16384)
+    assert L.geometry(512) == (64, 64, 256, 4 * 16384 + 4 * 2048 + 4 * 64 + 64) and L.geometry(384) == (64, 64, 256, 3 * 16384)
     assert L.geometry(384, L.FA_DTYPE_FP64)[:3] == (64, 16, 256)
 
 

@@ -321,15 +321,47 @@ def test_dtiled_kernel_in_bounds(B, H, L, d, dq, dv):
     q_rows = np.minimum(L - q_tile0, 64)
     q.check(2 * (bh * L * D + q_tile0 * D), q_rows * ROWD, "Q descriptor")
     ntiles = -(-L // 64)
+    pshare = d == 512  # fa_fwd_dtp_kernel: V chunk c holds dv/2 columns of each half of d
     for t in range(ntiles):
         valid = min(64, L - t * 64)
-        for alloc, dt in ((k, dq), (v, dv)):
-            for c in range(D // dt):
-                base = bh * L * ROWD + t * 64 * ROWD + c * 2 * dt
-                alloc.check(base, (valid - 1) * ROWD + 2 * dt, f"chunk t={t} c={c}")
+        for c in range(D // dq):
+            k.check(bh * L * ROWD + t * 64 * ROWD + c * 2 * dq, (valid - 1) * ROWD + 2 * dq, f"K chunk t={t} c={c}")
+        for c in range(D // dv):
+            if pshare:
+                base, span = bh * L * ROWD + t * 64 * ROWD + c * dv, (valid - 1) * ROWD + 2 * (D // 2 + dv // 2)
+            else:
+                base, span = bh * L * ROWD + t * 64 * ROWD + c * 2 * dv, (valid - 1) * ROWD + 2 * dv
+            v.check(base, span, f"V chunk t={t} c={c}")
     rows = q_tile0[:, None] + np.arange(64)[None, :]
     live = rows < L
     o.check(np.where(live, 2 * (bh[:, None] * L * D + rows * D), 0), np.where(live, ROWD, 0), "O row store")
+
+
+@pytest.mark.parametrize("dv", [32, 64, 128])
+def test_dtiled_pair_columns(dv):
+    """fa_fwd_dtp_kernel (d = 512): V chunk c's image takes its first dv/2 columns from the first
+    half of d and the rest from the second (the DMA source offsets of src_off); wave h of a pair
+    reads image column blocks h * dv/32 .. and stores them as its O^T blocks c * dv/32 + j of
+    half h.  Every column of V is read once per tile, into the O^T block that owns it, and the
+    two waves of a pair store every column of both of its query blocks once."""
+    D = 512
+    seen = {}
+    for c in range(D // dv):
+        for ch in range(dv // 8):  # 16-byte chunks of the image row
+            col = 8 * ch + (D // 2 - dv // 2 if 8 * ch >= dv // 2 else 0)
+            gcol = c * dv // 2 + col  # the descriptor starts at column c * dv/2
+            for x in range(8):
+                assert gcol + x not in seen
+                seen[gcol + x] = (c, ch)
+    assert sorted(seen) == list(range(D))
+    bph = dv // 32  # 16-column blocks per half of a chunk
+    for h in (0, 1):
+        for c in range(D // dv):
+            for j in range(bph):
+                jj = h * bph + j  # image column block
+                b = c * bph + j  # O^T block of this half
+                image_cols = [seen_c for seen_c, (cc, ch) in seen.items() if cc == c and ch // 2 == jj]
+                assert sorted(image_cols) == list(range(h * D // 2 + 16 * b, h * D // 2 + 16 * b + 16))
 
 
 def chain_items(nitems, grid):
