@@ -22,7 +22,7 @@ def main():
     vals, kernels = {}, set()
     for f in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if not re.search(r"fa_fwd(16|16_chain|_dt)?_kernel", r["Kernel_Name"]):
+            if not re.search(r"fa_fwd(16|16_chain|_dtp?)?_kernel", r["Kernel_Name"]):
                 continue
             kernels.add(r["Kernel_Name"].split("(")[0])
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
