@@ -705,6 +705,25 @@ def test_tiled_d_wide(gpu, d, dtype, L):
     assert torch.equal(ops.attention_v2(qd, kd, vd, kv_tiles_per_block=4), outs[0])
 
 
+@pytest.mark.parametrize("L", [1, 17, 65, 130, 1000])
+def test_tiled_d_pair_ragged(gpu, L):
+    """fa_fwd_dtp_kernel (d = 512, wave pairs sharing P through LDS) at ragged lengths: a pair
+    whose two query blocks straddle Lq (one wave's rows valid, its partner's past the end), a
+    single key, partial last key tiles -- every tile pair within the oracle's gates and the
+    64-column-chunk output bitwise equal to the 128-column one."""
+    from exploring_flash_attention_amd import ops
+    q, k, v = _inputs(1, 2, L, 512, torch.bfloat16, seed=L)
+    ref = _ref(q, k, v)
+    qd, kd, vd = q.cuda(), k.cuda(), v.cuda()
+    with ops.launched_kernels() as kl:
+        o128 = ops.attention_tiled_d(qd, kd, vd, 128, 128)
+    o64 = ops.attention_tiled_d(qd, kd, vd, 64, 32)
+    torch.cuda.synchronize()
+    assert kl == [f"fa_fwd_dtp_kernel [grid {2 * -(-L // 64)}]"]
+    _gate(o128, ref, torch.bfloat16)
+    assert torch.equal(o64, o128)
+
+
 @pytest.mark.parametrize("d", [384, 512])
 def test_tiled_d_wide_fp64(gpu, d):
     """The fp64 d-tiled kernel (Q chunks re-read per KV tile, as the reference's kernel) holds
