@@ -293,7 +293,7 @@ def test_launched_kernels_reported(gpu):
     assert run(ops.attention_v1, 2, 2, 1024, 32) == ["fa_fwd_kernel<final> [grid 32]"]
     assert run(ops.attention_v1, 1, 2, 1000, 128) == ["fa_fwd_kernel<final> [grid 16]"]
     assert run(lambda q, k, v: ops.attention_tiled_d(q, k, v, 64, 64), 1, 2, 256, 384) == ["fa_fwd_dt_kernel [grid 8]"]
-    assert run(lambda q, k, v: ops.attention_tiled_d(q, k, v, 64, 64), 1, 2, 256, 512) == ["fa_fwd_dtp_kernel [grid 8]"]
+    assert run(lambda q, k, v: ops.attention_tiled_d(q, k, v, 64, 64), 1, 2, 256, 512) == ["fa_fwd_dt_kernel<paired> [grid 8]"]
     kl = run(lambda q, k, v: ops.attention_v2(q, k, v, 4), 1, 2, 4096, 128)
     assert len(kl) == 1 and kl[0].startswith("fa_fwd16_kernel<fused split, in-kernel combine> [grid ")
     with ops.launched_kernels() as kl:

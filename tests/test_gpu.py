@@ -707,7 +707,7 @@ def test_tiled_d_wide(gpu, d, dtype, L):
 
 @pytest.mark.parametrize("L", [1, 17, 65, 130, 1000])
 def test_tiled_d_pair_ragged(gpu, L):
-    """fa_fwd_dtp_kernel (d = 512, wave pairs sharing P through LDS) at ragged lengths: a pair
+    """fa_fwd_dt_kernel<paired> (d = 512, wave pairs sharing P through LDS) at ragged lengths: a pair
     whose two query blocks straddle Lq (one wave's rows valid, its partner's past the end), a
     single key, partial last key tiles -- every tile pair within the oracle's gates and the
     64-column-chunk output bitwise equal to the 128-column one."""
@@ -719,7 +719,7 @@ def test_tiled_d_pair_ragged(gpu, L):
         o128 = ops.attention_tiled_d(qd, kd, vd, 128, 128)
     o64 = ops.attention_tiled_d(qd, kd, vd, 64, 32)
     torch.cuda.synchronize()
-    assert kl == [f"fa_fwd_dtp_kernel [grid {2 * -(-L // 64)}]"]
+    assert kl == [f"fa_fwd_dt_kernel<paired> [grid {2 * -(-L // 64)}]"]
     _gate(o128, ref, torch.bfloat16)
     assert torch.equal(o64, o128)
 

@@ -321,7 +321,7 @@ def test_dtiled_kernel_in_bounds(B, H, L, d, dq, dv):
     q_rows = np.minimum(L - q_tile0, 64)
     q.check(2 * (bh * L * D + q_tile0 * D), q_rows * ROWD, "Q descriptor")
     ntiles = -(-L // 64)
-    pshare = d == 512  # fa_fwd_dtp_kernel: V chunk c holds dv/2 columns of each half of d
+    pshare = d == 512  # the paired form of fa_fwd_dt_kernel: V chunk c holds dv/2 columns of each half of d
     for t in range(ntiles):
         valid = min(64, L - t * 64)
         for c in range(D // dq):
@@ -339,7 +339,7 @@ def test_dtiled_kernel_in_bounds(B, H, L, d, dq, dv):
 
 @pytest.mark.parametrize("dv", [32, 64, 128])
 def test_dtiled_pair_columns(dv):
-    """fa_fwd_dtp_kernel (d = 512): V chunk c's image takes its first dv/2 columns from the first
+    """fa_fwd_dt_kernel, paired (d = 512): V chunk c's image takes its first dv/2 columns from the first
     half of d and the rest from the second (the DMA source offsets of src_off); wave h of a pair
     reads image column blocks h * dv/32 .. and stores them as its O^T blocks c * dv/32 + j of
     half h.  Every column of V is read once per tile, into the O^T block that owns it, and the
