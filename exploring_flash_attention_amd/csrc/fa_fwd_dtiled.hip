@@ -29,7 +29,9 @@
 //     NSLOT-1 chunks ahead of use: the chunk stream K(t,0..) V(t,0..) K(t+1,0..) ... runs one
 //     raw barrier per chunk, the DMA of the next chunk issued right after the barrier that
 //     retires the previous chunk's slot;
-//   * registers: d = 384 and 512 both fit 256 (two workgroups per CU: 224 / 252 VGPRs).
+//   * registers: d = 384 and 512 both fit 256 (two workgroups per CU: 224 / 246-256 VGPRs);
+//   * d = 512 pairs the waves (PAIR, below): P^T shared through LDS, each wave's P.V on half of
+//     d for both query blocks of its pair -- half the V^T reads per MFMA.
 #include "fa_device.hpp"
 #include "fa_dtiled_stream.hpp"
 
